@@ -1,0 +1,11 @@
+"""blazingmq_amd -- MI355X-native replacement for BlazingMQ's per-message
+CRC32C integrity-checksum path (bmqp::Crc32c and its batch callers).
+
+The product is the C-ABI library ``lib/libbmqcrc.so`` (HIP kernels for gfx950
++ host dispatcher); this package is its Python host-side mirror.
+"""
+from .crc32c import (Blob, BmqCrcError, Crc32c, calculate_batch_multi,  # noqa: F401
+                     device_count, fill_synthetic, kernel_timing)
+
+__all__ = ["Blob", "BmqCrcError", "Crc32c", "calculate_batch_multi", "device_count",
+           "fill_synthetic", "kernel_timing"]

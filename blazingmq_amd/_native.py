@@ -1,0 +1,80 @@
+"""ctypes binding to the in-tree C-ABI library ``lib/libbmqcrc.so``.
+
+There is no pure-Python or CPU substitute for the batch path: if the library
+is missing this module raises at import, and the batch entry point returns
+BMQCRC_ENODEV (raised as ``BmqCrcError``) when no MI355X is usable.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libbmqcrc.so")
+
+BMQCRC_OK = 0
+BMQCRC_EIO = -5
+BMQCRC_ENOMEM = -12
+BMQCRC_ENODEV = -19
+BMQCRC_EINVAL = -22
+BMQCRC_F_DEVICE_PTRS = 0x1
+BMQCRC_F_ASYNC = 0x2
+BMQCRC_F_TIME_KERNEL = 0x4
+
+
+class BmqCrcError(RuntimeError):
+    def __init__(self, rc, msg):
+        super().__init__("bmqcrc error %d: %s" % (rc, msg))
+        self.rc = rc
+
+
+class Opts(ctypes.Structure):
+    _fields_ = [("struct_size", ctypes.c_uint32), ("device", ctypes.c_int32),
+                ("stream", ctypes.c_void_p), ("flags", ctypes.c_uint32),
+                ("seg_bytes", ctypes.c_uint32)]
+
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError("libbmqcrc.so not built (%s); run `python -c \"import __graft_entry__ as g; "
+                      "g.build()\"` first" % LIB_PATH)
+
+lib = ctypes.CDLL(LIB_PATH)
+_u32, _u64, _vp, _int = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int
+
+lib.bmqcrc_crc32c.restype = _u32
+lib.bmqcrc_crc32c.argtypes = [_vp, _u32, _u32]
+lib.bmqcrc_crc32c_blob.restype = _u32
+lib.bmqcrc_crc32c_blob.argtypes = [ctypes.POINTER(_vp), ctypes.POINTER(_u32), _u32, _u32]
+lib.bmqcrc_combine.restype = _u32
+lib.bmqcrc_combine.argtypes = [_u32, _u32, _u64]
+lib.bmqcrc_crc32c_batch.restype = _int
+lib.bmqcrc_crc32c_batch.argtypes = [_vp, _u64, _vp, _vp, _vp, _vp, _u64, ctypes.POINTER(Opts)]
+lib.bmqcrc_crc32c_batch_multi.restype = _int
+lib.bmqcrc_crc32c_batch_multi.argtypes = [_vp, _u64, _vp, _vp, _vp, _vp, _u64, _vp, _int, _u32]
+lib.bmqcrc_reserve.restype = _int
+lib.bmqcrc_reserve.argtypes = [_int, _vp, _u64, _u64, _u32]
+lib.bmqcrc_fill_synthetic.restype = _int
+lib.bmqcrc_fill_synthetic.argtypes = [_vp, _u64, _u64, _u64, ctypes.POINTER(Opts)]
+lib.bmqcrc_kernel_timing.restype = _int
+lib.bmqcrc_kernel_timing.argtypes = [_int, _vp, ctypes.POINTER(ctypes.c_double),
+                                     ctypes.POINTER(_u32)]
+lib.bmqcrc_device_count.restype = _int
+lib.bmqcrc_device_count.argtypes = []
+lib.bmqcrc_last_error.restype = ctypes.c_char_p
+lib.bmqcrc_last_error.argtypes = []
+lib.bmqcrc_version.restype = _u32
+lib.bmqcrc_version.argtypes = []
+
+
+def check(rc):
+    if rc != BMQCRC_OK:
+        raise BmqCrcError(rc, lib.bmqcrc_last_error().decode(errors="replace"))
+    return rc
+
+
+def make_opts(device=-1, stream=None, flags=0, seg_bytes=0):
+    o = Opts()
+    o.struct_size = ctypes.sizeof(Opts)
+    o.device = device
+    o.stream = stream
+    o.flags = flags
+    o.seg_bytes = seg_bytes
+    return o

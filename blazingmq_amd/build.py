@@ -1,0 +1,91 @@
+"""Build the in-tree native artefacts.
+
+* ``blazingmq_amd/lib/libbmqcrc.so`` -- the product: HIP kernels for gfx950
+  (hipcc --offload-arch=gfx950) + the C-ABI host code (include/bmqcrc.h).
+* ``oracle/lib/liboracle_crc32c.so`` -- the CPU checker (test infrastructure).
+* ``blazingmq_amd/lib/bmqp_selftest`` -- the C++ drop-in (bmqp::Crc32c) test
+  driver, linked against libbmqcrc.so.
+
+hipcc cross-compiles gfx950 code objects without a GPU present.
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "lib")
+ORACLE = os.path.join(ROOT, "oracle")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+
+PRODUCT_SOURCES = ["crc32c_kernels.hip", "bmqcrc_host.cpp", "crc32c_cpu.cpp", "bmqp_crc32c.cpp"]
+PRODUCT_DEPS = ["bmqcrc_internal.h", "crc32c_consts.h"]
+
+
+def _run(cmd):
+    print("+", " ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+
+
+def _stale(target, sources):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(s) > t for s in sources)
+
+
+def build_consts():
+    gen = os.path.join(ROOT, "tools", "gen_crc_consts.py")
+    out = os.path.join(CSRC, "crc32c_consts.h")
+    if _stale(out, [gen]):
+        _run([sys.executable, gen, out])
+
+
+def build_product(force=False):
+    os.makedirs(LIB, exist_ok=True)
+    build_consts()
+    target = os.path.join(LIB, "libbmqcrc.so")
+    srcs = [os.path.join(CSRC, s) for s in PRODUCT_SOURCES]
+    deps = srcs + [os.path.join(CSRC, d) for d in PRODUCT_DEPS] + [
+        os.path.join(ROOT, "include", "bmqcrc.h"), os.path.join(ROOT, "include", "bmqp_crc32c.h")]
+    if force or _stale(target, deps):
+        objs = []
+        for s in srcs:
+            o = os.path.join(LIB, os.path.basename(s) + ".o")
+            cmd = [HIPCC, "-O3", "-fPIC", "-std=c++17", "-Wall", "-I" + os.path.join(ROOT, "include"),
+                   "-c", s, "-o", o]
+            if s.endswith(".hip"):
+                cmd[1:1] = ["-x", "hip", "--offload-arch=" + ARCH, "-munsafe-fp-atomics"]
+            _run(cmd)
+            objs.append(o)
+        _run([HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, *objs, "-o", target,
+              "-lpthread"])
+        for o in objs:
+            os.remove(o)
+    selftest = os.path.join(LIB, "bmqp_selftest")
+    st_src = os.path.join(ROOT, "tests", "cpp", "bmqp_crc32c_selftest.cpp")
+    if os.path.exists(st_src) and (force or _stale(selftest, [st_src, target])):
+        _run(["g++", "-O2", "-std=c++17", "-I" + os.path.join(ROOT, "include"), st_src,
+              "-o", selftest, "-L" + LIB, "-lbmqcrc", "-Wl,-rpath,$ORIGIN"])
+    return target
+
+
+def build_oracle(force=False):
+    out_dir = os.path.join(ORACLE, "lib")
+    os.makedirs(out_dir, exist_ok=True)
+    src = os.path.join(ORACLE, "crc32c_oracle.c")
+    target = os.path.join(out_dir, "liboracle_crc32c.so")
+    if force or _stale(target, [src]):
+        _run(["gcc", "-O3", "-fPIC", "-shared", "-pthread", "-Wall", "-Wextra", src, "-o", target])
+    return target
+
+
+def build_all(force=False):
+    build_oracle(force)
+    return build_product(force)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)

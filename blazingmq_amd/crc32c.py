@@ -1,0 +1,207 @@
+"""Host-side mirror of ``bmqp::Crc32c`` (reference:
+/root/reference/src/groups/bmq/bmqp/bmqp_crc32c.h:225-257) plus the batched
+MI355X entry point.
+
+    Crc32c.calculate(data, crc=Crc32c.k_NULL_CRC32C)      -> int   (CPU, like the reference)
+    Crc32c.calculate_blob(blob, crc=...)                    -> int   (CPU, bmqp_crc32c.cpp:47-67)
+    Crc32c.calculate_batch(arena, offsets, lengths, seeds)  -> out   (GPU only)
+
+``calculate_batch`` accepts torch tensors resident on an MI355X (no copies;
+enqueued on torch's current stream) or host buffers (numpy / bytes), which the
+library stages through HBM.  It never computes on the CPU: without a usable
+GPU it raises ``BmqCrcError`` (BMQCRC_ENODEV).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _native
+from ._native import BmqCrcError  # noqa: F401  (re-export)
+
+
+class Blob:
+    """Minimal stand-in for ``bdlbb::Blob``: an ordered list of data buffers.
+
+    Mirrors the members bmqp::Crc32c uses: ``num_data_buffers()``,
+    ``buffer(i)``, ``last_data_buffer_length()``.
+    """
+
+    def __init__(self, buffers=()):
+        self._buffers = [bytes(b) for b in buffers]
+        self._last_len = len(self._buffers[-1]) if self._buffers else 0
+
+    def append_data_buffer(self, buf):
+        self._buffers.append(bytes(buf))
+        self._last_len = len(self._buffers[-1])
+
+    def set_last_data_buffer_length(self, n):
+        self._last_len = n
+
+    def num_data_buffers(self):
+        return len(self._buffers)
+
+    def buffer(self, i):
+        return self._buffers[i]
+
+    def last_data_buffer_length(self):
+        return self._last_len
+
+
+def _as_bytes_ptr(data):
+    if data is None:
+        return None, 0, None
+    if isinstance(data, (bytes, bytearray, memoryview)):
+        buf = (ctypes.c_char * len(data)).from_buffer_copy(bytes(data))
+        return ctypes.cast(buf, ctypes.c_void_p), len(data), buf
+    arr = np.ascontiguousarray(data).view(np.uint8).reshape(-1)
+    return ctypes.c_void_p(arr.ctypes.data), arr.size, arr
+
+
+class Crc32c:
+    """``bmqp::Crc32c`` (bmqp_crc32c.h:225-257)."""
+
+    k_NULL_CRC32C = 0
+
+    @staticmethod
+    def calculate(data, crc=0, length=None):
+        """CRC32-C of ``data`` (bytes-like / numpy), continuing from ``crc``.
+
+        ``data=None`` requires ``length`` 0 (bmqp_crc32c.h:242-243).
+        """
+        ptr, n, keep = _as_bytes_ptr(data)
+        if length is not None:
+            if length > n:
+                raise ValueError("length exceeds buffer")
+            n = length
+        if ptr is None and n:
+            raise ValueError("null data with non-zero length")
+        r = _native.lib.bmqcrc_crc32c(ptr, n, crc & 0xFFFFFFFF)
+        del keep
+        return r
+
+    @staticmethod
+    def calculate_blob(blob, crc=0):
+        """CRC32-C over the data buffers of ``blob`` (bmqp_crc32c.cpp:47-67)."""
+        nb = blob.num_data_buffers()
+        if nb == 0:
+            return crc & 0xFFFFFFFF
+        keeps, ptrs, lens = [], (ctypes.c_void_p * nb)(), (ctypes.c_uint32 * nb)()
+        for i in range(nb):
+            b = blob.buffer(i)
+            n = len(b) if i < nb - 1 else blob.last_data_buffer_length()
+            p, _, k = _as_bytes_ptr(b)
+            keeps.append(k)
+            ptrs[i] = p
+            lens[i] = n
+        return _native.lib.bmqcrc_crc32c_blob(ptrs, lens, nb, crc & 0xFFFFFFFF)
+
+    @staticmethod
+    def combine(crc_a, crc_b, len_b):
+        return _native.lib.bmqcrc_combine(crc_a & 0xFFFFFFFF, crc_b & 0xFFFFFFFF, len_b)
+
+    @staticmethod
+    def calculate_batch(arena, offsets, lengths, seeds=None, out=None, *, seg_bytes=0,
+                        device=None, stream=None, sync=True, time_kernel=False):
+        """Batched CRC32-C of messages ``arena[offsets[i] : offsets[i]+lengths[i]]``.
+
+        torch CUDA tensors: ``arena`` uint8, ``offsets`` int64, ``lengths`` /
+        ``seeds`` / ``out`` int32 (read as u32) on one device; the call is
+        enqueued on ``stream`` (default: torch's current stream) and
+        ``out`` (int32 tensor) is returned.  Host arrays: numpy in, numpy
+        ``uint32`` out.
+        """
+        try:
+            import torch
+        except ImportError:  # pragma: no cover
+            torch = None
+        if torch is not None and isinstance(arena, torch.Tensor) and arena.is_cuda:
+            return _batch_torch(torch, arena, offsets, lengths, seeds, out, seg_bytes, stream,
+                                sync, time_kernel)
+        return _batch_host(arena, offsets, lengths, seeds, out, seg_bytes, device)
+
+
+def _batch_torch(torch, arena, offsets, lengths, seeds, out, seg_bytes, stream, sync,
+                 time_kernel=False):
+    dev = arena.device
+    n = offsets.numel()
+    for name, t, dt in (("offsets", offsets, torch.int64), ("lengths", lengths, torch.int32)):
+        if not (isinstance(t, torch.Tensor) and t.device == dev and t.dtype == dt
+                and t.is_contiguous()):
+            raise TypeError("%s must be a contiguous %s tensor on %s" % (name, dt, dev))
+    if lengths.numel() != n:
+        raise ValueError("offsets/lengths size mismatch")
+    if seeds is not None and (seeds.device != dev or seeds.dtype != torch.int32
+                              or seeds.numel() != n):
+        raise TypeError("seeds must be an int32 tensor of n elements on %s" % dev)
+    if arena.dtype != torch.uint8 or not arena.is_contiguous():
+        raise TypeError("arena must be a contiguous uint8 tensor")
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+    if stream is None:
+        stream = torch.cuda.current_stream(dev)
+    flags = _native.BMQCRC_F_DEVICE_PTRS | (0 if sync else _native.BMQCRC_F_ASYNC)
+    if time_kernel:
+        flags |= _native.BMQCRC_F_TIME_KERNEL
+    o = _native.make_opts(device=dev.index if dev.index is not None else -1,
+                          stream=stream.cuda_stream, flags=flags, seg_bytes=seg_bytes)
+    _native.check(_native.lib.bmqcrc_crc32c_batch(
+        arena.data_ptr(), arena.numel(), offsets.data_ptr(), lengths.data_ptr(),
+        seeds.data_ptr() if seeds is not None else None, out.data_ptr(), n, ctypes.byref(o)))
+    return out
+
+
+def _batch_host(arena, offsets, lengths, seeds, out, seg_bytes, device):
+    a = np.frombuffer(bytes(arena), dtype=np.uint8) if isinstance(
+        arena, (bytes, bytearray, memoryview)) else np.ascontiguousarray(arena).view(np.uint8)
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    ln = np.ascontiguousarray(lengths, dtype=np.uint32)
+    if off.shape != ln.shape:
+        raise ValueError("offsets/lengths size mismatch")
+    sd = None if seeds is None else np.ascontiguousarray(seeds, dtype=np.uint32)
+    res = np.empty(off.size, dtype=np.uint32) if out is None else out
+    o = _native.make_opts(device=-1 if device is None else device, seg_bytes=seg_bytes)
+    _native.check(_native.lib.bmqcrc_crc32c_batch(
+        a.ctypes.data if a.size else None, a.size, off.ctypes.data, ln.ctypes.data,
+        sd.ctypes.data if sd is not None else None, res.ctypes.data, off.size, ctypes.byref(o)))
+    return res
+
+
+def calculate_batch_multi(arena, offsets, lengths, seeds=None, devices=None, seg_bytes=0):
+    """Host-buffer batch sharded byte-balanced over several GPUs of this process."""
+    a = np.ascontiguousarray(arena).view(np.uint8)
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    ln = np.ascontiguousarray(lengths, dtype=np.uint32)
+    sd = None if seeds is None else np.ascontiguousarray(seeds, dtype=np.uint32)
+    res = np.empty(off.size, dtype=np.uint32)
+    if devices is None:
+        devices = list(range(device_count()))
+    dv = (ctypes.c_int * len(devices))(*devices)
+    _native.check(_native.lib.bmqcrc_crc32c_batch_multi(
+        a.ctypes.data, a.size, off.ctypes.data, ln.ctypes.data,
+        sd.ctypes.data if sd is not None else None, res.ctypes.data, off.size, dv, len(devices),
+        seg_bytes))
+    return res
+
+
+def fill_synthetic(tensor, seed, stream=None, begin=0):
+    """Fill a CUDA uint8 tensor with bytes [begin, begin+numel) of synthetic stream ``seed``."""
+    import torch
+    if stream is None:
+        stream = torch.cuda.current_stream(tensor.device)
+    o = _native.make_opts(device=tensor.device.index, stream=stream.cuda_stream,
+                          flags=_native.BMQCRC_F_ASYNC)
+    _native.check(_native.lib.bmqcrc_fill_synthetic(tensor.data_ptr(), tensor.numel(), seed,
+                                                    begin, ctypes.byref(o)))
+    return tensor
+
+
+def kernel_timing(device, stream):
+    """(total_ms, count) of fold kernels timed with time_kernel=True since the last query."""
+    tot, cnt = ctypes.c_double(), ctypes.c_uint32()
+    _native.check(_native.lib.bmqcrc_kernel_timing(device, stream.cuda_stream, ctypes.byref(tot),
+                                                  ctypes.byref(cnt)))
+    return tot.value, cnt.value
+
+
+def device_count():
+    return _native.lib.bmqcrc_device_count()

@@ -1,0 +1,513 @@
+// bmqcrc_host.cpp -- C ABI implementation (include/bmqcrc.h).
+//
+// Device context, per-(device, stream) workspaces, host<->device staging and
+// multi-GPU sharding around the HIP kernels in crc32c_kernels.hip.  The batch
+// path is GPU-only: with no usable device it returns BMQCRC_ENODEV and never
+// computes on the CPU.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <utility>
+#include <vector>
+
+#include "../../include/bmqcrc.h"
+#include "bmqcrc_internal.h"
+
+namespace bmqcrc {
+uint32_t cpu_crc32c(const void* data, uint32_t length, uint32_t crc);
+uint32_t cpu_combine(uint32_t crcA, uint32_t crcB, uint64_t lenB);
+}  // namespace bmqcrc
+
+using namespace bmqcrc;
+
+namespace {
+
+thread_local std::string t_err;
+
+int fail(int rc, const std::string& msg)
+{
+    t_err = msg;
+    return rc;
+}
+
+#define HIP_TRY(expr)                                                                       \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess) {                                                             \
+            return fail(e_ == hipErrorOutOfMemory ? BMQCRC_ENOMEM : BMQCRC_EIO,             \
+                        std::string(#expr ": ") + hipGetErrorString(e_));                   \
+        }                                                                                   \
+    } while (0)
+
+struct DevBuf {
+    void* p = nullptr;
+    uint64_t bytes = 0;
+    int ensure(uint64_t want)
+    {
+        if (want <= bytes) {
+            return 0;
+        }
+        if (p) {
+            (void)hipFree(p);
+            p = nullptr;
+            bytes = 0;
+        }
+        want = std::max<uint64_t>(want, 256);
+        HIP_TRY(hipMalloc(&p, want));
+        bytes = want;
+        return 0;
+    }
+    ~DevBuf()
+    {
+        if (p) {
+            (void)hipFree(p);
+        }
+    }
+};
+
+// Planner + staging scratch for one (device, stream).
+struct Workspace {
+    std::mutex mu;
+    DevBuf seg_first, block_sum, seg2msg, ctrl;
+    // host-pointer staging
+    DevBuf arena, offsets, lengths, seeds, out;
+    // BMQCRC_F_TIME_KERNEL: event pairs around k_fold not yet reported
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> timing, spare;
+    ~Workspace()
+    {
+        for (auto& v : {timing, spare}) {
+            for (auto& e : v) {
+                (void)hipEventDestroy(e.first);
+                (void)hipEventDestroy(e.second);
+            }
+        }
+    }
+};
+
+struct DeviceState {
+    int num_cus = 0;
+    hipStream_t own_stream = nullptr;
+};
+
+std::mutex g_mu;
+std::map<std::pair<int, void*>, std::unique_ptr<Workspace>> g_ws;
+std::map<int, DeviceState> g_dev;
+
+int device_count_raw()
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        return 0;
+    }
+    return n;
+}
+
+int resolve_device(int dev, int* out)
+{
+    const int n = device_count_raw();
+    if (n <= 0) {
+        return fail(BMQCRC_ENODEV, "no HIP device available (batch CRC32C runs only on the GPU)");
+    }
+    if (dev < 0) {
+        HIP_TRY(hipGetDevice(&dev));
+    }
+    if (dev >= n) {
+        return fail(BMQCRC_EINVAL, "device ordinal out of range");
+    }
+    *out = dev;
+    return 0;
+}
+
+int device_state(int dev, DeviceState** st)
+{
+    std::lock_guard<std::mutex> g(g_mu);
+    DeviceState& s = g_dev[dev];
+    if (s.num_cus == 0) {
+        hipDeviceProp_t prop;
+        HIP_TRY(hipGetDeviceProperties(&prop, dev));
+        if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+            return fail(BMQCRC_ENODEV, std::string("device is ") + prop.gcnArchName +
+                                           ", this library is built for gfx950 (MI355X) only");
+        }
+        s.num_cus = prop.multiProcessorCount;
+        HIP_TRY(hipSetDevice(dev));
+        HIP_TRY(hipStreamCreateWithFlags(&s.own_stream, hipStreamNonBlocking));
+    }
+    *st = &s;
+    return 0;
+}
+
+Workspace* workspace(int dev, void* stream)
+{
+    std::lock_guard<std::mutex> g(g_mu);
+    auto& w = g_ws[std::make_pair(dev, stream)];
+    if (!w) {
+        w.reset(new Workspace());
+    }
+    return w.get();
+}
+
+uint64_t max_segs_for(uint64_t n, uint64_t arena_bytes, uint32_t seg)
+{
+    // Sum over messages of ceil(len/seg) <= n + total_len/seg.  For
+    // non-overlapping messages total_len <= arena_bytes; segments past this
+    // bound (overlapping batches) are resolved by binary search in-kernel.
+    return n + arena_bytes / seg + 64;
+}
+
+int plan_ws(Workspace* w, uint64_t n, uint64_t arena_bytes, uint32_t seg, BatchArgs* a)
+{
+    const uint64_t nblocks = (n + kPlanBlock - 1) / kPlanBlock;
+    const uint64_t max_segs = max_segs_for(n, arena_bytes, seg);
+    int rc;
+    if ((rc = w->seg_first.ensure(4 * std::max<uint64_t>(n, 1))) ||
+        (rc = w->block_sum.ensure(8 * std::max<uint64_t>(nblocks, 1))) ||
+        (rc = w->seg2msg.ensure(4 * max_segs)) || (rc = w->ctrl.ensure(sizeof(PlanCtrl)))) {
+        return rc;
+    }
+    a->seg_first = (uint32_t*)w->seg_first.p;
+    a->block_sum = (uint32_t*)w->block_sum.p;
+    a->seg2msg = (uint32_t*)w->seg2msg.p;
+    a->ctrl = (PlanCtrl*)w->ctrl.p;
+    a->nblocks = (uint32_t)nblocks;
+    a->max_segs = max_segs;
+    return 0;
+}
+
+int check_seg(uint32_t* seg)
+{
+    if (*seg == 0) {
+        *seg = kDefaultSegBytes;
+    }
+    if (*seg % kLine != 0 || *seg < 256 || *seg > (1u << 30)) {
+        return fail(BMQCRC_EINVAL, "seg_bytes must be a multiple of 128 in [256, 2^30]");
+    }
+    return 0;
+}
+
+int batch_one(int dev, void* user_stream, uint32_t flags, uint32_t seg, const void* arena,
+              uint64_t arena_bytes, const uint64_t* offsets, const uint32_t* lengths,
+              const uint32_t* seeds, uint32_t* out, uint64_t n)
+{
+    DeviceState* st = nullptr;
+    int rc = device_state(dev, &st);
+    if (rc) {
+        return rc;
+    }
+    HIP_TRY(hipSetDevice(dev));
+    hipStream_t s = user_stream ? (hipStream_t)user_stream : st->own_stream;
+    Workspace* w = workspace(dev, user_stream);
+    std::lock_guard<std::mutex> g(w->mu);
+
+    BatchArgs a;
+    memset(&a, 0, sizeof(a));
+    a.n = n;
+    a.seg_bytes = seg;
+    if ((rc = plan_ws(w, n, arena_bytes, seg, &a))) {
+        return rc;
+    }
+    const bool dev_ptrs = (flags & BMQCRC_F_DEVICE_PTRS) != 0;
+    if (dev_ptrs) {
+        a.arena = (const uint8_t*)arena;
+        a.offsets = offsets;
+        a.lengths = lengths;
+        a.seeds = seeds;
+        a.out = out;
+    } else {
+        if ((rc = w->arena.ensure(arena_bytes + 16)) || (rc = w->offsets.ensure(8 * n)) ||
+            (rc = w->lengths.ensure(4 * n)) || (rc = w->out.ensure(4 * n)) ||
+            (seeds && (rc = w->seeds.ensure(4 * n)))) {
+            return rc;
+        }
+        HIP_TRY(hipMemcpyAsync(w->arena.p, arena, arena_bytes, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(w->offsets.p, offsets, 8 * n, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(w->lengths.p, lengths, 4 * n, hipMemcpyHostToDevice, s));
+        if (seeds) {
+            HIP_TRY(hipMemcpyAsync(w->seeds.p, seeds, 4 * n, hipMemcpyHostToDevice, s));
+        }
+        a.arena = (const uint8_t*)w->arena.p;
+        a.offsets = (const uint64_t*)w->offsets.p;
+        a.lengths = (const uint32_t*)w->lengths.p;
+        a.seeds = seeds ? (const uint32_t*)w->seeds.p : nullptr;
+        a.out = (uint32_t*)w->out.p;
+    }
+    void* ev0 = nullptr;
+    void* ev1 = nullptr;
+    if (flags & BMQCRC_F_TIME_KERNEL) {
+        std::pair<hipEvent_t, hipEvent_t> ev;
+        if (!w->spare.empty()) {
+            ev = w->spare.back();
+            w->spare.pop_back();
+        } else {
+            HIP_TRY(hipEventCreate(&ev.first));
+            HIP_TRY(hipEventCreate(&ev.second));
+        }
+        w->timing.push_back(ev);
+        ev0 = (void*)ev.first;
+        ev1 = (void*)ev.second;
+    }
+    if (bmqcrc_launch_batch(&a, (void*)s, st->num_cus, ev0, ev1) != 0) {
+        return fail(BMQCRC_EIO, std::string("kernel launch failed: ") +
+                                    hipGetErrorString(hipGetLastError()));
+    }
+    if (!dev_ptrs) {
+        HIP_TRY(hipMemcpyAsync(out, w->out.p, 4 * n, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    } else if (!(flags & BMQCRC_F_ASYNC)) {
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t bmqcrc_crc32c(const void* data, uint32_t length, uint32_t crc)
+{
+    return bmqcrc::cpu_crc32c(data, length, crc);
+}
+
+uint32_t bmqcrc_crc32c_blob(const void* const* bufs, const uint32_t* lens, uint32_t nbuf,
+                            uint32_t crc)
+{
+    // bmqp_crc32c.cpp:47-67: an empty blob returns crc; otherwise chain.
+    for (uint32_t i = 0; i < nbuf; ++i) {
+        crc = bmqcrc::cpu_crc32c(bufs[i], lens[i], crc);
+    }
+    return crc;
+}
+
+uint32_t bmqcrc_combine(uint32_t crcA, uint32_t crcB, uint64_t lenB)
+{
+    return bmqcrc::cpu_combine(crcA, crcB, lenB);
+}
+
+int bmqcrc_crc32c_batch(const void* arena, uint64_t arena_bytes, const uint64_t* offsets,
+                        const uint32_t* lengths, const uint32_t* seeds, uint32_t* out,
+                        uint64_t n, const bmqcrc_opts* opts)
+{
+    t_err.clear();
+    if (n == 0) {
+        return 0;
+    }
+    if (!offsets || !lengths || !out || (!arena && arena_bytes)) {
+        return fail(BMQCRC_EINVAL, "null pointer argument");
+    }
+    if (n > 0xFFFFFFFFull) {
+        return fail(BMQCRC_EINVAL, "at most 2^32-1 messages per batch");
+    }
+    bmqcrc_opts o;
+    memset(&o, 0, sizeof(o));
+    o.device = -1;
+    if (opts) {
+        memcpy(&o, opts, std::min<size_t>(sizeof(o), opts->struct_size ? opts->struct_size
+                                                                        : sizeof(o)));
+    }
+    uint32_t seg = o.seg_bytes;
+    int rc = check_seg(&seg);
+    if (rc) {
+        return rc;
+    }
+    int dev;
+    if ((rc = resolve_device(o.device, &dev))) {
+        return rc;
+    }
+    if (!(o.flags & BMQCRC_F_DEVICE_PTRS)) {
+        // Host pointers: bounds check here (device arrays are trusted).
+        for (uint64_t i = 0; i < n; ++i) {
+            if (offsets[i] > arena_bytes || lengths[i] > arena_bytes - offsets[i]) {
+                return fail(BMQCRC_EINVAL, "message " + std::to_string(i) +
+                                               " lies outside [arena, arena+arena_bytes)");
+            }
+        }
+    }
+    return batch_one(dev, o.stream, o.flags, seg, arena, arena_bytes, offsets, lengths, seeds,
+                     out, n);
+}
+
+int bmqcrc_crc32c_batch_multi(const void* arena, uint64_t arena_bytes, const uint64_t* offsets,
+                              const uint32_t* lengths, const uint32_t* seeds, uint32_t* out,
+                              uint64_t n, const int* devices, int ndev, uint32_t seg_bytes)
+{
+    t_err.clear();
+    if (n == 0) {
+        return 0;
+    }
+    if (ndev < 1 || !offsets || !lengths || !out || !arena) {
+        return fail(BMQCRC_EINVAL, "bad arguments");
+    }
+    uint32_t seg = seg_bytes;
+    int rc = check_seg(&seg);
+    if (rc) {
+        return rc;
+    }
+    const int have = device_count_raw();
+    if (have <= 0) {
+        return fail(BMQCRC_ENODEV, "no HIP device available");
+    }
+    std::vector<int> devs(ndev);
+    for (int d = 0; d < ndev; ++d) {
+        devs[d] = devices ? devices[d] : d;
+        if (devs[d] < 0 || devs[d] >= have) {
+            return fail(BMQCRC_EINVAL, "device ordinal out of range");
+        }
+    }
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (offsets[i] > arena_bytes || lengths[i] > arena_bytes - offsets[i]) {
+            return fail(BMQCRC_EINVAL, "message outside arena");
+        }
+        total += lengths[i];
+    }
+    // Contiguous byte-balanced message slices; each device gets its own
+    // copy of the arena range its slice touches.
+    std::vector<uint64_t> cut(ndev + 1, n);
+    cut[0] = 0;
+    {
+        uint64_t acc = 0, i = 0;
+        for (int d = 1; d < ndev; ++d) {
+            const uint64_t target = total * (uint64_t)d / (uint64_t)ndev;
+            while (i < n && acc < target) {
+                acc += lengths[i++];
+            }
+            cut[d] = i;
+        }
+    }
+    std::vector<int> rcs(ndev, 0);
+    std::vector<std::string> errs(ndev);
+    std::vector<std::thread> th;
+    for (int d = 0; d < ndev; ++d) {
+        th.emplace_back([&, d]() {
+            const uint64_t lo = cut[d], hi = cut[d + 1];
+            if (lo >= hi) {
+                return;
+            }
+            uint64_t amin = UINT64_MAX, amax = 0;
+            for (uint64_t i = lo; i < hi; ++i) {
+                amin = std::min(amin, offsets[i]);
+                amax = std::max(amax, offsets[i] + lengths[i]);
+            }
+            if (amin > amax) {
+                amin = amax = 0;
+            }
+            std::vector<uint64_t> rel(hi - lo);
+            for (uint64_t i = lo; i < hi; ++i) {
+                rel[i - lo] = offsets[i] - amin;
+            }
+            rcs[d] = batch_one(devs[d], nullptr, 0, seg, (const uint8_t*)arena + amin, amax - amin,
+                               rel.data(), lengths + lo, seeds ? seeds + lo : nullptr, out + lo,
+                               hi - lo);
+            errs[d] = t_err;
+        });
+    }
+    for (auto& t : th) {
+        t.join();
+    }
+    for (int d = 0; d < ndev; ++d) {
+        if (rcs[d]) {
+            return fail(rcs[d], "device " + std::to_string(devs[d]) + ": " + errs[d]);
+        }
+    }
+    return 0;
+}
+
+int bmqcrc_reserve(int device, void* stream, uint64_t n_msgs, uint64_t arena_bytes,
+                   uint32_t seg_bytes)
+{
+    t_err.clear();
+    int dev, rc;
+    if ((rc = check_seg(&seg_bytes)) || (rc = resolve_device(device, &dev))) {
+        return rc;
+    }
+    DeviceState* st = nullptr;
+    if ((rc = device_state(dev, &st))) {
+        return rc;
+    }
+    HIP_TRY(hipSetDevice(dev));
+    Workspace* w = workspace(dev, stream);
+    std::lock_guard<std::mutex> g(w->mu);
+    BatchArgs a;
+    return plan_ws(w, n_msgs, arena_bytes, seg_bytes, &a);
+}
+
+int bmqcrc_fill_synthetic(void* dev_dst, uint64_t nbytes, uint64_t seed, uint64_t begin,
+                          const bmqcrc_opts* opts)
+{
+    t_err.clear();
+    int dev, rc;
+    if ((rc = resolve_device(opts ? opts->device : -1, &dev))) {
+        return rc;
+    }
+    if (((uintptr_t)dev_dst & 7u) || (begin & 7u)) {
+        return fail(BMQCRC_EINVAL, "destination and begin must be 8-byte aligned");
+    }
+    DeviceState* st = nullptr;
+    if ((rc = device_state(dev, &st))) {
+        return rc;
+    }
+    HIP_TRY(hipSetDevice(dev));
+    hipStream_t s = (opts && opts->stream) ? (hipStream_t)opts->stream : st->own_stream;
+    if (bmqcrc_launch_fill((uint8_t*)dev_dst, nbytes, seed, begin, (void*)s)) {
+        return fail(BMQCRC_EIO, "fill launch failed");
+    }
+    if (!(opts && (opts->flags & BMQCRC_F_ASYNC))) {
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    return 0;
+}
+
+int bmqcrc_kernel_timing(int device, void* stream, double* total_ms, uint32_t* count)
+{
+    t_err.clear();
+    int dev, rc;
+    if ((rc = resolve_device(device, &dev))) {
+        return rc;
+    }
+    HIP_TRY(hipSetDevice(dev));
+    Workspace* w = workspace(dev, stream);
+    std::lock_guard<std::mutex> g(w->mu);
+    double tot = 0;
+    uint32_t cnt = 0;
+    for (auto& e : w->timing) {
+        HIP_TRY(hipEventSynchronize(e.second));
+        float ms = 0;
+        HIP_TRY(hipEventElapsedTime(&ms, e.first, e.second));
+        tot += ms;
+        ++cnt;
+        w->spare.push_back(e);
+    }
+    w->timing.clear();
+    if (total_ms) {
+        *total_ms = tot;
+    }
+    if (count) {
+        *count = cnt;
+    }
+    return 0;
+}
+
+int bmqcrc_device_count(void)
+{
+    return device_count_raw();
+}
+
+const char* bmqcrc_last_error(void)
+{
+    return t_err.c_str();
+}
+
+uint32_t bmqcrc_version(void)
+{
+    return (1u << 16) | 0u;
+}
+
+}  // extern "C"

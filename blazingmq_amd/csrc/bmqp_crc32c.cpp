@@ -1,0 +1,49 @@
+// bmqp_crc32c.cpp -- bmqp::Crc32c over the bmqcrc C ABI.
+// Reference: /root/reference/src/groups/bmq/bmqp/bmqp_crc32c.cpp:39-67.
+#include "bmqp_crc32c.h"
+
+#include <stdint.h>
+
+namespace BloombergLP {
+namespace bmqp {
+
+const unsigned int Crc32c::k_NULL_CRC32C = BMQCRC_NULL_CRC32C;
+
+unsigned int Crc32c::calculate(const void* data, unsigned int length, unsigned int crc)
+{
+    return bmqcrc_crc32c(data, length, crc);
+}
+
+unsigned int Crc32c::calculate(const bdlbb::Blob& blob, unsigned int crc)
+{
+    // Same chaining as the reference: every buffer but the last in full, the
+    // last up to lastDataBufferLength(); no buffers -> crc unchanged.
+    const int numBuffers = blob.numDataBuffers();
+    if (numBuffers == 0) {
+        return crc;
+    }
+    for (int i = 0; i < numBuffers - 1; ++i) {
+        const bdlbb::BlobBuffer& buffer = blob.buffer(i);
+        crc = calculate(buffer.data(), static_cast<unsigned int>(buffer.size()), crc);
+    }
+    return calculate(blob.buffer(numBuffers - 1).data(),
+                     static_cast<unsigned int>(blob.lastDataBufferLength()), crc);
+}
+
+int Crc32c::calculateBatch(const void* arena,
+                           unsigned long long arenaBytes,
+                           const unsigned long long* offsets,
+                           const unsigned int* lengths,
+                           const unsigned int* seeds,
+                           unsigned int* crcs,
+                           unsigned long long count,
+                           const bmqcrc_opts* opts)
+{
+    static_assert(sizeof(unsigned long long) == sizeof(uint64_t), "u64");
+    static_assert(sizeof(unsigned int) == sizeof(uint32_t), "u32");
+    return bmqcrc_crc32c_batch(arena, arenaBytes, reinterpret_cast<const uint64_t*>(offsets),
+                               lengths, seeds, crcs, count, opts);
+}
+
+}  // namespace bmqp
+}  // namespace BloombergLP

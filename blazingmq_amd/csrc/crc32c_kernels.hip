@@ -1,0 +1,598 @@
+// crc32c_kernels.hip -- MI355X (gfx950) batched CRC32C.
+//
+// Replaces, for batches, the arithmetic behind
+//   bmqp::Crc32c::calculate(const void*, unsigned, unsigned)
+//   (/root/reference/src/groups/bmq/bmqp/bmqp_crc32c.cpp:41-45 -> BDE
+//   bdlde::Crc32c::calculate) with bit-exact CRC-32C (Castagnoli).
+//
+// Design (DESIGN.md sections 2-4):
+//   * A message is cut into segments of <= seg_bytes; one LANE owns one
+//     segment and folds it serially as a stream of 32-bit words.
+//   * The fold is table-less: the minimal polynomial of y = x^32 mod P,
+//     m(y) = y^32 + sum_{k in REL_TAPS} y^k, vanishes mod P, so the word
+//     stream is reduced modulo m(y) by a 17-tap Fibonacci recurrence over a
+//     32-word register ring -- 9 v_bitop3 (3-input XOR) per word, no
+//     carry-less multiply, no lookup table.
+//   * Only the last 32 remainder words get a real GF(2) reduction (Horner by
+//     x^32, 64 VALU/word), once per segment.
+//   * Bytes reach the lanes through LDS: per round a wave DMAs (LDS-DMA,
+//     global_load_lds_dwordx4) the next 128-byte line of each of its 64
+//     segments, 8 lanes per full 128-byte line (coalesced), with the piece
+//     order XOR-swizzled on the SOURCE address so that every owner lane's
+//     ds_read_b128 is bank-conflict free.  Two LDS slots per wave: round r+1
+//     is in flight while round r folds.
+//   * Per-segment raw remainders are moved to the message end with x^e mod P
+//     (e mod ord(x) = 2^31-1, which also un-shifts the zero padding) and
+//     XOR-combined into out[msg] (plain store for single-segment messages,
+//     global atomic XOR otherwise -- XOR is order independent, so results are
+//     deterministic).  The seed enters as ~seed XORed into the message's
+//     first 4 bytes; the final inversion is one XOR with 0xFFFFFFFF.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bmqcrc_internal.h"
+#include "crc32c_consts.h"
+
+namespace bmqcrc {
+
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const u32x4 lds_cu4;
+
+__constant__ uint32_t c_x2col[31][32] = BMQCRC_X2COL;
+
+// ------------------------------------------------------------ GF(2) helpers
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // a ^ b ^ c
+}
+
+__device__ __forceinline__ uint32_t xand(uint32_t acc, uint32_t mask, uint32_t col)
+{
+    return __builtin_amdgcn_bitop3_b32(acc, mask, col, 0x78);  // acc ^ (mask & col)
+}
+
+__device__ __forceinline__ uint32_t bitmask(uint32_t v, int t)
+{
+    return (uint32_t)__builtin_amdgcn_sbfe((int)v, t, 1);  // 0 or ~0
+}
+
+// v * x^32 mod P (reflected), 64 VALU.
+__device__ __forceinline__ uint32_t mul_y(uint32_t v)
+{
+    constexpr uint32_t col[32] = BMQCRC_YCOL;
+    uint32_t a0 = 0, a1 = 0;
+#pragma unroll
+    for (int t = 0; t < 32; t += 2) {
+        a0 = xand(a0, bitmask(v, t), col[t]);
+        a1 = xand(a1, bitmask(v, t + 1), col[t + 1]);
+    }
+    return a0 ^ a1;
+}
+
+// v * x^e mod P (reflected), e in [0, 2^31-1).  Column tables are uniform
+// (scalar loads); bits no lane needs are skipped wave-uniformly.
+__device__ uint32_t mul_xpow(uint32_t v, uint32_t e)
+{
+    for (int j = 0; j < 31; ++j) {
+        const bool bit = (e >> j) & 1u;
+        if (__ballot(bit) == 0) {
+            continue;
+        }
+        uint32_t a0 = 0, a1 = 0;
+#pragma unroll
+        for (int t = 0; t < 32; t += 2) {
+            a0 = xand(a0, bitmask(v, t), c_x2col[j][t]);
+            a1 = xand(a1, bitmask(v, t + 1), c_x2col[j][t + 1]);
+        }
+        v = bit ? (a0 ^ a1) : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint32_t mersenne31(uint64_t x)
+{
+    // x mod (2^31 - 1)
+    x = (x & 0x7fffffffull) + (x >> 31);
+    x = (x & 0x7fffffffull) + (x >> 31);
+    x = (x & 0x7fffffffull) + (x >> 31);
+    return (x >= 0x7fffffffull) ? (uint32_t)(x - 0x7fffffffull) : (uint32_t)x;
+}
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        v = max(v, (uint32_t)__shfl_xor((int)v, o));
+    }
+    return __builtin_amdgcn_readfirstlane(v);
+}
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src)
+{
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t rfl64(uint64_t v)
+{
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// ---------------------------------------------------- fold ring (m(y) taps)
+constexpr int kTaps[BMQCRC_REL_NTAPS] = BMQCRC_REL_TAPS;
+constexpr int kNTaps = BMQCRC_REL_NTAPS;
+
+// One full round = 32 words = one turn of the ring.  Ring slot d holds the
+// quotient word Q_i of the latest stream index i == d (mod 32):
+//   Q_i = m_i ^ sum_{k in taps} Q_{i-32+k}
+// Slot (d+k)&31 is still the previous round's word when d+k < 32 and this
+// round's when d+k >= 32, exactly the recurrence.
+__device__ __forceinline__ void fold_round(uint32_t (&q)[32], const uint32_t (&m)[32])
+{
+#pragma unroll
+    for (int d = 0; d < 32; ++d) {
+        uint32_t acc = m[d];
+        int i = 0;
+#pragma unroll
+        for (; i + 1 < kNTaps; i += 2) {
+            acc = xor3(acc, q[(d + kTaps[i]) & 31], q[(d + kTaps[i + 1]) & 31]);
+        }
+        if (i < kNTaps) {
+            acc ^= q[(d + kTaps[i]) & 31];
+        }
+        q[d] = acc;
+    }
+}
+
+// Final round: the last 32 words are the remainder coefficients.  Taps that
+// would reach this round's (non-existent) quotient words are dropped; the
+// remainder is then reduced by Horner with x^32:  raw = sum R_d y^(32-d).
+__device__ __forceinline__ uint32_t tail_round(const uint32_t (&q)[32], const uint32_t (&m)[32])
+{
+    uint32_t c = 0;
+#pragma unroll
+    for (int d = 0; d < 32; ++d) {
+        uint32_t acc = m[d];
+        uint32_t pend = 0;
+        bool have = false;
+#pragma unroll
+        for (int i = 0; i < kNTaps; ++i) {
+            if (d + kTaps[i] <= 31) {
+                if (have) {
+                    acc = xor3(acc, pend, q[d + kTaps[i]]);
+                    have = false;
+                } else {
+                    pend = q[d + kTaps[i]];
+                    have = true;
+                }
+            }
+        }
+        if (have) {
+            acc ^= pend;
+        }
+        c = mul_y(c ^ acc);
+    }
+    return c;
+}
+
+__device__ __forceinline__ uint32_t bytemask(int nbytes)
+{
+    return nbytes >= 4 ? 0xffffffffu : ((1u << (8 * nbytes)) - 1u);
+}
+
+// Zero bytes outside [S, E) and XOR the seed word into bytes [S, S+4) of the
+// first segment.  sR = S - p0, eR = E - p0 (clamped), p0 = round's first byte.
+__device__ __forceinline__ void mask_round(uint32_t (&m)[32], int sR, int eR, bool first, uint32_t c0)
+{
+#pragma unroll
+    for (int d = 0; d < 32; ++d) {
+        const int lo = min(max(sR - 4 * d, 0), 4);
+        const int hi = min(max(eR - 4 * d, 0), 4);
+        const uint32_t keep = (hi > lo) ? (bytemask(hi) & ~bytemask(lo)) : 0u;
+        const int o = sR - 4 * d;
+        uint32_t inj = 0;
+        if (first) {
+            if (o >= 0 && o < 4) {
+                inj = c0 << (8 * o);
+            } else if (o < 0 && o > -4) {
+                inj = c0 >> (8 * (-o));
+            }
+        }
+        m[d] = (m[d] & keep) ^ inj;
+    }
+}
+
+// Issue one round of LDS-DMA: 8 x global_load_lds_dwordx4 (8 x 1 KiB), each
+// covering 8 segments x one full 128-byte line.  M0 = LDS destination.
+__device__ __forceinline__ void dma_round(uint32_t lds_dst, const uint64_t (&dbase)[8],
+                                          const uint32_t (&dlim)[8], uint32_t r)
+{
+    uint64_t s[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        s[i] = dbase[i] + ((uint64_t)min(r, dlim[i]) << 7);
+    }
+    uint32_t keep;
+    asm volatile(
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %1\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %2, off\n\t"
+        "s_add_u32 m0, m0, 0x400\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %3, off\n\t"
+        "s_add_u32 m0, m0, 0x400\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %4, off\n\t"
+        "s_add_u32 m0, m0, 0x400\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %5, off\n\t"
+        "s_add_u32 m0, m0, 0x400\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %6, off\n\t"
+        "s_add_u32 m0, m0, 0x400\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %7, off\n\t"
+        "s_add_u32 m0, m0, 0x400\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %8, off\n\t"
+        "s_add_u32 m0, m0, 0x400\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %9, off\n\t"
+        "s_mov_b32 m0, %0\n\t"
+        : "=&s"(keep)
+        : "s"(lds_dst), "v"(s[0]), "v"(s[1]), "v"(s[2]), "v"(s[3]), "v"(s[4]), "v"(s[5]),
+          "v"(s[6]), "v"(s[7])
+        : "memory", "scc");
+}
+
+// Binary search: last message i with seg_first[i] <= g (rare overflow path).
+__device__ uint32_t find_msg(const uint32_t* seg_first, uint64_t n, uint32_t g)
+{
+    uint64_t lo = 0, hi = n;  // invariant: seg_first[lo] <= g < seg_first[hi] (hi==n: inf)
+    while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (seg_first[mid] <= g) {
+            lo = mid;
+        } else {
+            hi = mid;
+        }
+    }
+    return (uint32_t)lo;
+}
+
+__global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t wave_lds = (uint32_t)(uintptr_t)(lds_u8*)lds + wave * (kSlots * kSlotBytes);
+
+    const uint32_t total = a.ctrl->total_segs;
+    const uint32_t identity = a.ctrl->identity;
+    const uint32_t ngroups = (total + 63u) / 64u;
+    const uint32_t SEG = a.seg_bytes;
+    const uint64_t arena = (uint64_t)(uintptr_t)a.arena;
+
+    const uint32_t rd_off = (uint32_t)lane * 128u + (((uint32_t)lane >> 1) & 7u) * 16u;
+
+    for (uint32_t g = blockIdx.x * kWavesPerBlock + wave; g < ngroups;
+         g += gridDim.x * kWavesPerBlock) {
+        // ---------------------------------------------------- descriptor
+        const uint32_t seg = g * 64u + (uint32_t)lane;
+        const bool valid = seg < total;
+        uint32_t msg = 0, len = 0, seed = 0, k = 0;
+        uint64_t off = 0;
+        if (valid) {
+            msg = identity ? seg
+                           : (seg < a.max_segs ? a.seg2msg[seg] : find_msg(a.seg_first, a.n, seg));
+            off = a.offsets[msg];
+            len = a.lengths[msg];
+            seed = a.seeds ? a.seeds[msg] : 0u;
+            k = seg - a.seg_first[msg];
+        }
+        const uint32_t nseg = valid ? (len - 1u) / SEG + 1u : 0u;
+        const uint64_t mstart = arena + off;
+        const uint64_t mend = mstart + len;
+        const uint64_t S = (k == 0) ? mstart : ((mstart + (uint64_t)k * SEG) & ~127ull);
+        const uint64_t E = (k + 1 == nseg) ? mend : ((mstart + (uint64_t)(k + 1) * SEG) & ~127ull);
+        const bool first = valid && k == 0;
+        const bool single = valid && nseg == 1;
+        const uint64_t L0 = S & ~127ull;
+        const uint64_t need_end = (first && E < S + 4) ? S + 4 : E;
+        const uint32_t nl = valid ? (uint32_t)((need_end - L0 + 127u) >> 7) : 0u;
+        const uint32_t nl_data = valid ? (uint32_t)((E - L0 + 127u) >> 7) : 0u;
+        const uint32_t R = wave_max(nl);
+
+        // ------------------------------------------ DMA source per instruction
+        const uint64_t dummy = rfl64(L0);  // lane 0 always holds a valid segment here
+        uint64_t dbase[8];
+        uint32_t dlim[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int src = 8 * i + (lane >> 3);
+            const uint64_t l0 = shfl64(L0, src);
+            const uint32_t nd = (uint32_t)__shfl((int)nl_data, src);
+            const uint32_t p = ((uint32_t)lane & 7u) ^ ((4u * i + ((uint32_t)lane >> 4)) & 7u);
+            dbase[i] = nd ? l0 + 16u * p : dummy;
+            dlim[i] = nd ? nd - 1u : 0u;
+        }
+
+        // ------------------------------------------------------ fold rounds
+        uint32_t q[32];
+#pragma unroll
+        for (int d = 0; d < 32; ++d) {
+            q[d] = 0;
+        }
+        uint32_t crc = 0;
+        const uint32_t c0 = ~seed;
+        const uint64_t inj_end = first ? S + 4 : S;
+
+        dma_round(wave_lds, dbase, dlim, 0);
+        if (R > 1) {
+            dma_round(wave_lds + kSlotBytes, dbase, dlim, 1);
+        }
+        for (uint32_t r = 0; r < R; ++r) {
+            const uint32_t slot = wave_lds + (r & 1u) * kSlotBytes;
+            if (r + 1 < R) {
+                asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            uint32_t m[32];
+#pragma unroll
+            for (int kk = 0; kk < 8; ++kk) {
+                const u32x4 v = *(lds_cu4*)(uintptr_t)(slot + (rd_off ^ (16u * kk)));
+                m[4 * kk + 0] = v.x;
+                m[4 * kk + 1] = v.y;
+                m[4 * kk + 2] = v.z;
+                m[4 * kk + 3] = v.w;
+            }
+            if (r + 2 < R) {
+                dma_round(slot, dbase, dlim, r + 2);
+            }
+            const uint64_t p0 = L0 + ((uint64_t)r << 7);
+            if (r < nl && (p0 < inj_end || p0 + 128u > E)) {
+                const int64_t sr = (int64_t)(S - p0);
+                const int64_t er = (int64_t)(E - p0);
+                const int sR = (int)(sr < -8 ? -8 : (sr > 136 ? 136 : sr));
+                const int eR = (int)(er < -8 ? -8 : (er > 136 ? 136 : er));
+                mask_round(m, sR, eR, first, c0);
+            }
+            if (r + 1 < nl) {
+                fold_round(q, m);
+            } else if (r + 1 == nl) {
+                crc = tail_round(q, m);
+            }
+        }
+
+        // ------------------------------------------------ move + combine
+        if (valid) {
+            const uint64_t stream_end = L0 + ((uint64_t)nl << 7);
+            const uint64_t padE = stream_end - E;
+            const uint64_t after = mend - E;
+            const uint32_t e = mersenne31(8ull * after + 8ull * 0x7fffffffull - 8ull * padE);
+            uint32_t contrib = mul_xpow(crc, e);
+            if (first) {
+                contrib ^= 0xffffffffu;
+            }
+            if (single) {
+                a.out[msg] = contrib;
+            } else {
+                atomicXor(&a.out[msg], contrib);
+            }
+        } else {
+            (void)mul_xpow(0u, 0u);  // keep the wave's ballots converged
+        }
+    }
+}
+
+// ---------------------------------------------------------------- planner
+__global__ __launch_bounds__(kPlanBlock) void k_plan_count(BatchArgs a)
+{
+    __shared__ uint32_t wsum[kPlanBlock / 64];
+    __shared__ uint32_t wnon1[kPlanBlock / 64];
+    const uint64_t i = (uint64_t)blockIdx.x * kPlanBlock + threadIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t ns = 0;
+    if (i < a.n) {
+        const uint32_t len = a.lengths[i];
+        ns = len ? (len - 1u) / a.seg_bytes + 1u : 0u;
+        a.out[i] = len ? 0u : (a.seeds ? a.seeds[i] : 0u);
+    }
+    const uint64_t non1_mask = __ballot(i < a.n && ns != 1u);
+    uint32_t x = ns;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+        if (lane >= o) {
+            x += y;
+        }
+    }
+    if (lane == 63) {
+        wsum[wave] = x;
+        wnon1[wave] = (uint32_t)__popcll(non1_mask);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = 0, non1 = 0;
+        for (int w = 0; w < kPlanBlock / 64; ++w) {
+            const uint32_t t = wsum[w];
+            wsum[w] = run;
+            run += t;
+            non1 += wnon1[w];
+        }
+        a.block_sum[blockIdx.x] = run;
+        a.block_sum[a.nblocks + blockIdx.x] = non1;
+    }
+    __syncthreads();
+    if (i < a.n) {
+        a.seg_first[i] = x - ns + wsum[wave];
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_plan_scan(BatchArgs a)
+{
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t carry_s, non1_s;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (threadIdx.x == 0) {
+        carry_s = 0;
+        non1_s = 0;
+    }
+    __syncthreads();
+    for (uint32_t base = 0; base < a.nblocks; base += 1024) {
+        const uint32_t j = base + threadIdx.x;
+        const uint32_t v = j < a.nblocks ? a.block_sum[j] : 0u;
+        const uint32_t nn = j < a.nblocks ? a.block_sum[a.nblocks + j] : 0u;
+        if (nn) {
+            atomicAdd(&non1_s, nn);
+        }
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+            if (lane >= o) {
+                x += y;
+            }
+        }
+        if (lane == 63) {
+            wsum[wave] = x;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t run = 0;
+            for (int w = 0; w < 16; ++w) {
+                const uint32_t t = wsum[w];
+                wsum[w] = run;
+                run += t;
+            }
+        }
+        __syncthreads();
+        const uint32_t carry = carry_s;
+        if (j < a.nblocks) {
+            a.block_sum[j] = carry + wsum[wave] + x - v;
+        }
+        __syncthreads();
+        if (threadIdx.x == 1023) {
+            carry_s = carry + wsum[wave] + x;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        a.ctrl->total_segs = carry_s;
+        a.ctrl->identity = (non1_s == 0) ? 1u : 0u;
+        a.ctrl->ngroups = (carry_s + 63u) / 64u;
+        a.ctrl->pad = 0;
+    }
+}
+
+__global__ void k_plan_fix(BatchArgs a)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < a.n) {
+        a.seg_first[i] += a.block_sum[i / kPlanBlock];
+    }
+}
+
+__global__ void k_plan_emit(BatchArgs a)
+{
+    if (a.ctrl->identity) {
+        return;
+    }
+    const uint64_t total = a.ctrl->total_segs;
+    const uint64_t lim = total < a.max_segs ? total : a.max_segs;
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < lim;
+         g += (uint64_t)gridDim.x * blockDim.x) {
+        a.seg2msg[g] = find_msg(a.seg_first, a.n, (uint32_t)g);
+    }
+}
+
+// ------------------------------------------------------- synthetic payload
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+// byte i of the payload stream = byte (i % 8) of splitmix64(seed*golden + i/8);
+// identical to oracle_fill_payload().  dst must be 8-byte aligned.
+__global__ void k_fill(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t begin)
+{
+    const uint64_t nw = nbytes >> 3;
+    const uint64_t key = seed * 0x9E3779B97F4A7C15ull + (begin >> 3);
+    uint64_t* d64 = (uint64_t*)dst;
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw;
+         w += (uint64_t)gridDim.x * blockDim.x) {
+        d64[w] = splitmix64(key + w);
+    }
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < (nbytes & 7)) {
+        const uint64_t g = (nw << 3) + t;
+        dst[g] = (uint8_t)(splitmix64(key + (g >> 3)) >> (8 * (g & 7)));  // begin % 8 == 0
+    }
+}
+
+}  // namespace bmqcrc
+
+using namespace bmqcrc;
+
+extern "C" int bmqcrc_launch_batch(const BatchArgs* a, void* stream, int num_cus, void* ev_start,
+                                   void* ev_stop)
+{
+    hipStream_t s = (hipStream_t)stream;
+    if (a->n == 0) {
+        return 0;
+    }
+    hipLaunchKernelGGL(k_plan_count, dim3(a->nblocks), dim3(kPlanBlock), 0, s, *a);
+    hipLaunchKernelGGL(k_plan_scan, dim3(1), dim3(1024), 0, s, *a);
+    hipLaunchKernelGGL(k_plan_fix, dim3(a->nblocks), dim3(kPlanBlock), 0, s, *a);
+    uint64_t emit_blocks = (a->max_segs + 255) / 256;
+    if (emit_blocks > 4096) {
+        emit_blocks = 4096;
+    }
+    hipLaunchKernelGGL(k_plan_emit, dim3((unsigned)emit_blocks), dim3(256), 0, s, *a);
+    const uint64_t max_groups = (a->max_segs + 63) / 64;
+    uint64_t grid = (max_groups + kWavesPerBlock - 1) / kWavesPerBlock;
+    const uint64_t cap = (uint64_t)(num_cus > 0 ? num_cus : 256) * 2;
+    if (grid > cap) {
+        grid = cap;
+    }
+    if (grid < 1) {
+        grid = 1;
+    }
+    if (ev_start) {
+        (void)hipEventRecord((hipEvent_t)ev_start, s);
+    }
+    hipLaunchKernelGGL(k_fold, dim3((unsigned)grid), dim3(kWavesPerBlock * 64), 0, s, *a);
+    if (ev_stop) {
+        (void)hipEventRecord((hipEvent_t)ev_stop, s);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" int bmqcrc_launch_fill(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t begin,
+                                  void* stream)
+{
+    if (nbytes == 0) {
+        return 0;
+    }
+    uint64_t blocks = (nbytes / 8 + 255) / 256;
+    if (blocks > 65536) {
+        blocks = 65536;
+    }
+    if (blocks < 1) {
+        blocks = 1;
+    }
+    hipLaunchKernelGGL(k_fill, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, dst,
+                       nbytes, seed, begin);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}

@@ -1,0 +1,124 @@
+/* bmqcrc.h -- C ABI of the MI355X CRC32C library (libbmqcrc.so).
+ *
+ * Drop-in boundary for BlazingMQ's per-message CRC32C path.  Every entry point
+ * takes plain pointers and sizes; no HIP or torch types cross the ABI.
+ *
+ * Reference interfaces replaced (paths relative to /root/reference):
+ *   bmqcrc_crc32c        bmqp::Crc32c::calculate(const void*, unsigned, unsigned)
+ *                        src/groups/bmq/bmqp/bmqp_crc32c.h:244-246, .cpp:41-45
+ *   bmqcrc_crc32c_blob   bmqp::Crc32c::calculate(const bdlbb::Blob&, unsigned)
+ *                        src/groups/bmq/bmqp/bmqp_crc32c.h:255-256, .cpp:47-67
+ *   BMQCRC_NULL_CRC32C   bmqp::Crc32c::k_NULL_CRC32C (bmqp_crc32c.h:233, .cpp:39)
+ *   bmqcrc_crc32c_batch  the per-message loops that call the above once per
+ *                        message: PutEventBuilder::packMessage
+ *                        (src/groups/bmq/bmqp/bmqp_puteventbuilder.cpp:302,320,400,413)
+ *                        and FileStore::recoverMessages
+ *                        (src/groups/mqb/mqbs/mqbs_filestore.cpp:2603-2624);
+ *                        one call CRCs a whole batch on an MI355X.
+ *   bmqcrc_combine       GF(2) shift-combine crc(A||B) from crc(A), crc(B), |B|
+ *                        (used to stitch segments; no reference equivalent).
+ *
+ * Semantics of every CRC entry point are those of bmqp::Crc32c: reflected
+ * CRC-32C (Castagnoli, 0x1EDC6F41), `crc` is the finalised CRC of the
+ * preceding bytes (0 = k_NULL_CRC32C), calculate(p, 0, crc) == crc.
+ *
+ * Scalar entry points run on the host CPU (like the reference: one small
+ * buffer per call is latency-bound; a GPU round trip would be ~10^4 x slower).
+ * The batch entry points run ONLY on the GPU: they never fall back to the CPU
+ * and return BMQCRC_ENODEV when no MI355X is usable.
+ */
+#ifndef BMQCRC_H
+#define BMQCRC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BMQCRC_NULL_CRC32C 0u
+
+/* Return codes: 0 on success, negative errno-style values on failure. */
+#define BMQCRC_OK 0
+#define BMQCRC_EIO (-5)
+#define BMQCRC_ENOMEM (-12)
+#define BMQCRC_ENODEV (-19)
+#define BMQCRC_EINVAL (-22)
+
+/* bmqcrc_opts.flags */
+#define BMQCRC_F_DEVICE_PTRS 0x1u /* arena/offsets/lengths/seeds/out are device pointers */
+#define BMQCRC_F_ASYNC 0x2u       /* device ptrs only: return after enqueueing on stream */
+#define BMQCRC_F_TIME_KERNEL 0x4u /* record HIP events around the fold kernel (see bmqcrc_kernel_timing) */
+
+typedef struct bmqcrc_opts {
+    uint32_t struct_size; /* sizeof(bmqcrc_opts) */
+    int32_t device;       /* HIP device ordinal; -1 = current device */
+    void* stream;         /* hipStream_t; NULL = library-owned stream of that device */
+    uint32_t flags;       /* BMQCRC_F_* */
+    uint32_t seg_bytes;   /* segment size in bytes, multiple of 128; 0 = default (16384) */
+} bmqcrc_opts;
+
+/* ---- scalar (host CPU) -------------------------------------------------- */
+
+/* bmqp::Crc32c::calculate(data, length, crc).  data may be NULL iff length==0. */
+uint32_t bmqcrc_crc32c(const void* data, uint32_t length, uint32_t crc);
+
+/* bmqp::Crc32c::calculate(blob, crc): CRC of the concatenation of nbuf
+ * buffers, chained from crc.  nbuf == 0 returns crc. */
+uint32_t bmqcrc_crc32c_blob(const void* const* bufs, const uint32_t* lens, uint32_t nbuf,
+                            uint32_t crc);
+
+/* crc(A||B) given crc(A), crc(B) (both finalised, seed 0 for B) and |B|. */
+uint32_t bmqcrc_combine(uint32_t crcA, uint32_t crcB, uint64_t lenB);
+
+/* ---- batch (MI355X) ----------------------------------------------------- */
+
+/* out[i] = calculate(arena + offsets[i], lengths[i], seeds ? seeds[i] : 0)
+ * for i < n.  Messages may sit anywhere in [arena, arena + arena_bytes) at any
+ * byte alignment and may overlap.  With BMQCRC_F_DEVICE_PTRS all five arrays
+ * are device memory of opts->device (inputs "device resident"); otherwise they
+ * are host memory and the library stages them through HBM.  Returns 0,
+ * BMQCRC_EINVAL, BMQCRC_ENODEV, BMQCRC_ENOMEM or BMQCRC_EIO. */
+int bmqcrc_crc32c_batch(const void* arena, uint64_t arena_bytes, const uint64_t* offsets,
+                        const uint32_t* lengths, const uint32_t* seeds, uint32_t* out,
+                        uint64_t n, const bmqcrc_opts* opts);
+
+/* Host-pointer batch sharded over `ndev` devices: messages are split into
+ * contiguous byte-balanced slices, one per device, each on its own stream,
+ * with no inter-device communication.  devices==NULL means 0..ndev-1. */
+int bmqcrc_crc32c_batch_multi(const void* arena, uint64_t arena_bytes, const uint64_t* offsets,
+                              const uint32_t* lengths, const uint32_t* seeds, uint32_t* out,
+                              uint64_t n, const int* devices, int ndev, uint32_t seg_bytes);
+
+/* Pre-size the device workspace of (device, stream) for batches of up to
+ * n_msgs messages over arena_bytes bytes, so later calls allocate nothing
+ * (required before capturing bmqcrc_crc32c_batch into a hipGraph). */
+int bmqcrc_reserve(int device, void* stream, uint64_t n_msgs, uint64_t arena_bytes,
+                   uint32_t seg_bytes);
+
+/* Fill nbytes of device memory with bytes [begin, begin + nbytes) of the
+ * deterministic synthetic payload stream `seed` used by the benchmarks
+ * (splitmix64 counter stream; begin must be a multiple of 8). */
+int bmqcrc_fill_synthetic(void* dev_dst, uint64_t nbytes, uint64_t seed, uint64_t begin,
+                          const bmqcrc_opts* opts);
+
+/* Sum and count of fold-kernel durations (ms, HIP events on the launch
+ * stream) recorded by calls with BMQCRC_F_TIME_KERNEL on (device, stream)
+ * since the previous query; waits for those events, then resets. */
+int bmqcrc_kernel_timing(int device, void* stream, double* total_ms, uint32_t* count);
+
+/* Number of usable HIP devices (0 when none). */
+int bmqcrc_device_count(void);
+
+/* Message for the last failing call on this thread ("" if none). */
+const char* bmqcrc_last_error(void);
+
+/* ABI version: (major << 16) | minor. */
+uint32_t bmqcrc_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BMQCRC_H */

@@ -1,0 +1,105 @@
+"""CPU oracle for the CRC32C path -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this package, and only as the checker / reported CPU baseline; the product
+(blazingmq_amd/) never imports it.  See crc32c_oracle.c for what it restates.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "liboracle_crc32c.so")
+
+VARIANTS = {"hw": 0, "hw_serial": 1, "sw": 2, "bitwise": 3}
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            import subprocess
+            import sys
+            subprocess.check_call([sys.executable, os.path.join(_HERE, "..", "blazingmq_amd",
+                                                                "build.py")])
+        L = ctypes.CDLL(LIB_PATH)
+        u32, u64, vp = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p
+        for f in ("oracle_crc32c_bitwise", "oracle_crc32c_sw", "oracle_crc32c_hw",
+                  "oracle_crc32c_hw_serial"):
+            getattr(L, f).restype = u32
+            getattr(L, f).argtypes = [vp, u32, u32]
+        L.oracle_crc32c_combine.restype = u32
+        L.oracle_crc32c_combine.argtypes = [u32, u32, u64]
+        L.oracle_crc32c_blob.restype = u32
+        L.oracle_crc32c_blob.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(u32), u32, u32]
+        L.oracle_crc32c_batch.restype = ctypes.c_int
+        L.oracle_crc32c_batch.argtypes = [vp, vp, vp, vp, vp, ctypes.c_size_t, ctypes.c_int,
+                                          ctypes.c_int]
+        L.oracle_time_batch.restype = ctypes.c_double
+        L.oracle_time_batch.argtypes = [vp, vp, vp, vp, vp, ctypes.c_size_t, ctypes.c_int,
+                                        ctypes.c_int, ctypes.c_int]
+        L.oracle_fill_payload.restype = None
+        L.oracle_fill_payload.argtypes = [vp, u64, u64, u64]
+        L.oracle_have_sse42.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def _buf(data):
+    if isinstance(data, np.ndarray):
+        a = np.ascontiguousarray(data).view(np.uint8).reshape(-1)
+        return a, a.ctypes.data
+    b = bytes(data)
+    a = np.frombuffer(b, dtype=np.uint8) if b else np.zeros(1, np.uint8)
+    return a, a.ctypes.data
+
+
+def crc32c(data, crc=0, variant="bitwise"):
+    a, p = _buf(data)
+    n = len(data) if not isinstance(data, np.ndarray) else data.nbytes
+    return getattr(lib(), "oracle_crc32c_" + variant)(p, n, crc & 0xFFFFFFFF)
+
+
+def combine(a, b, len_b):
+    return lib().oracle_crc32c_combine(a, b, len_b)
+
+
+def blob(buffers, crc=0):
+    n = len(buffers)
+    keep = [_buf(b) for b in buffers]
+    ptrs = (ctypes.c_void_p * max(n, 1))(*[k[1] for k in keep])
+    lens = (ctypes.c_uint32 * max(n, 1))(*[len(b) for b in buffers])
+    return lib().oracle_crc32c_blob(ptrs, lens, n, crc)
+
+
+def batch(arena, offsets, lengths, seeds=None, nthreads=1, variant="hw"):
+    a = np.ascontiguousarray(arena).view(np.uint8)
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    ln = np.ascontiguousarray(lengths, dtype=np.uint32)
+    sd = None if seeds is None else np.ascontiguousarray(seeds, dtype=np.uint32)
+    out = np.empty(off.size, dtype=np.uint32)
+    lib().oracle_crc32c_batch(a.ctypes.data, off.ctypes.data, ln.ctypes.data,
+                              sd.ctypes.data if sd is not None else None, out.ctypes.data,
+                              off.size, nthreads, VARIANTS[variant])
+    return out
+
+
+def time_batch(arena, offsets, lengths, nthreads, variant="hw", reps=1):
+    a = np.ascontiguousarray(arena).view(np.uint8)
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    ln = np.ascontiguousarray(lengths, dtype=np.uint32)
+    out = np.empty(off.size, dtype=np.uint32)
+    t = lib().oracle_time_batch(a.ctypes.data, off.ctypes.data, ln.ctypes.data, None,
+                                out.ctypes.data, off.size, nthreads, VARIANTS[variant], reps)
+    return t, out
+
+
+def fill_payload(begin, nbytes, seed):
+    """Host copy of bytes [begin, begin+nbytes) of the synthetic stream `seed`."""
+    out = np.empty(nbytes, dtype=np.uint8)
+    if nbytes:
+        lib().oracle_fill_payload(out.ctypes.data, begin, nbytes, seed)
+    return out

@@ -1,0 +1,389 @@
+/*
+ * crc32c_oracle.c -- CPU restatement of the reference CRC32C path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the checker for the MI355X HIP
+ * path and the CPU baseline timed beside it in bench.py.  It is imported
+ * only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg;
+ * the shipped library (blazingmq_amd/) never links or calls it.
+ *
+ * What it restates
+ * ----------------
+ * bmqp::Crc32c::calculate(const void*, unsigned, unsigned crc)
+ *     /root/reference/src/groups/bmq/bmqp/bmqp_crc32c.cpp:41-45 forwards to
+ *     bdlde::Crc32c::calculate (BDE tag 4.39.0.0, pinned in
+ *     /root/reference/bin/build-ubuntu.sh:71; BDE is NOT vendored in the
+ *     reference and is absent from this image).  Semantics pinned by the
+ *     reference's own tests (bmqp_crc32c.t.cpp:282-390, 416-434, 598-671):
+ *       - CRC-32C (Castagnoli), reflected polynomial 0x82F63B78
+ *         (normal 0x1EDC6F41), register initialised to ~crc, result ~register;
+ *       - calculate(p, 0, c) == c, calculate(0, 0, c) == c;
+ *       - calculate(b, len_b, calculate(a, len_a)) == calculate(a||b).
+ * bmqp::Crc32c::calculate(const bdlbb::Blob&, unsigned crc)
+ *     bmqp_crc32c.cpp:47-67: chain the above over the blob's data buffers
+ *     (full size() for all but the last, lastDataBufferLength() for the
+ *     last); an empty blob returns crc.
+ *
+ * Variants (BASELINE.md section 2 -- BDE's own code cannot be built here, so
+ * these are the published algorithms BDE's implementation names follow):
+ *   oracle_crc32c_bitwise    bit-at-a-time definition (ground truth)
+ *   oracle_crc32c_sw         slicing-by-8 tables  (Crc32c_Impl::calculateSoftware)
+ *   oracle_crc32c_hw_serial  SSE4.2 crc32q serial (Crc32c_Impl::calculateHardwareSerial)
+ *   oracle_crc32c_hw         SSE4.2 3-way interleaved + GF(2) shift-combine
+ *                            (bdlde::Crc32c::calculate default)
+ * Parity of all variants is pinned by tests/golden/ (the reference's golden
+ * vectors) in tests/test_oracle_golden.py.
+ */
+#include <stddef.h>
+#include <stdint.h>
+#include <string.h>
+#include <pthread.h>
+#include <time.h>
+
+#if defined(__x86_64__)
+#include <cpuid.h>
+#include <nmmintrin.h>
+#define ORACLE_HAVE_X86 1
+#endif
+
+#define POLY 0x82F63B78u
+
+/* ---------------------------------------------------------------- bitwise */
+uint32_t oracle_crc32c_bitwise(const void *data, uint32_t len, uint32_t crc)
+{
+    const uint8_t *p = (const uint8_t *)data;
+    uint32_t c = ~crc;
+    for (uint32_t i = 0; i < len; ++i) {
+        c ^= p[i];
+        for (int k = 0; k < 8; ++k) {
+            c = (c >> 1) ^ (POLY & (0u - (c & 1u)));
+        }
+    }
+    return ~c;
+}
+
+/* ------------------------------------------------------------ slicing-by-8 */
+static uint32_t g_tab[8][256];
+static pthread_once_t g_tab_once = PTHREAD_ONCE_INIT;
+
+static void init_tables(void)
+{
+    for (uint32_t i = 0; i < 256; ++i) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; ++k) {
+            c = (c >> 1) ^ (POLY & (0u - (c & 1u)));
+        }
+        g_tab[0][i] = c;
+    }
+    for (uint32_t i = 0; i < 256; ++i) {
+        for (int t = 1; t < 8; ++t) {
+            uint32_t prev = g_tab[t - 1][i];
+            g_tab[t][i] = (prev >> 8) ^ g_tab[0][prev & 0xFF];
+        }
+    }
+}
+
+static uint32_t sw_raw(const uint8_t *p, size_t len, uint32_t c)
+{
+    while (len && ((uintptr_t)p & 7)) {
+        c = g_tab[0][(c ^ *p++) & 0xFF] ^ (c >> 8);
+        --len;
+    }
+    while (len >= 8) {
+        uint64_t w;
+        memcpy(&w, p, 8);
+        w ^= c;
+        c = g_tab[7][w & 0xFF] ^ g_tab[6][(w >> 8) & 0xFF] ^
+            g_tab[5][(w >> 16) & 0xFF] ^ g_tab[4][(w >> 24) & 0xFF] ^
+            g_tab[3][(w >> 32) & 0xFF] ^ g_tab[2][(w >> 40) & 0xFF] ^
+            g_tab[1][(w >> 48) & 0xFF] ^ g_tab[0][w >> 56];
+        p += 8;
+        len -= 8;
+    }
+    while (len--) {
+        c = g_tab[0][(c ^ *p++) & 0xFF] ^ (c >> 8);
+    }
+    return c;
+}
+
+uint32_t oracle_crc32c_sw(const void *data, uint32_t len, uint32_t crc)
+{
+    pthread_once(&g_tab_once, init_tables);
+    if (len == 0) {
+        return crc;
+    }
+    return ~sw_raw((const uint8_t *)data, len, ~crc);
+}
+
+/* ------------------------------------------------- GF(2) helpers (combine) */
+/* a * b mod P, reflected convention (bit 31 <-> x^0). */
+static uint32_t multmodp(uint32_t a, uint32_t b)
+{
+    uint32_t m = 1u << 31, p = 0;
+    for (;;) {
+        if (a & m) {
+            p ^= b;
+            if ((a & (m - 1)) == 0) {
+                break;
+            }
+        }
+        m >>= 1;
+        b = (b & 1) ? (b >> 1) ^ POLY : b >> 1;
+    }
+    return p;
+}
+
+/* x^(8*n) mod P by square-and-multiply. */
+static uint32_t x8nmodp(uint64_t n)
+{
+    uint32_t xp = 1u << 30; /* x^1 */
+    uint32_t p = 1u << 31;  /* x^0 */
+    uint64_t e = n * 8u;
+    while (e) {
+        if (e & 1) {
+            p = multmodp(xp, p);
+        }
+        xp = multmodp(xp, xp);
+        e >>= 1;
+    }
+    return p;
+}
+
+/* crc(A||B) from crc(A), crc(B), |B| (finalised CRCs, zlib-style). */
+uint32_t oracle_crc32c_combine(uint32_t crcA, uint32_t crcB, uint64_t lenB)
+{
+    return multmodp(x8nmodp(lenB), crcA) ^ crcB;
+}
+
+/* ---------------------------------------------------------------- SSE4.2 */
+static int g_have_sse42 = -1;
+
+int oracle_have_sse42(void)
+{
+#ifdef ORACLE_HAVE_X86
+    if (g_have_sse42 < 0) {
+        unsigned a, b, c, d;
+        g_have_sse42 = (__get_cpuid(1, &a, &b, &c, &d) && (c & bit_SSE4_2)) ? 1 : 0;
+    }
+    return g_have_sse42;
+#else
+    return 0;
+#endif
+}
+
+#ifdef ORACLE_HAVE_X86
+__attribute__((target("sse4.2"))) static uint32_t hw_raw(const uint8_t *p, size_t len, uint32_t c)
+{
+    uint64_t c64 = c;
+    while (len && ((uintptr_t)p & 7)) {
+        c64 = _mm_crc32_u8((uint32_t)c64, *p++);
+        --len;
+    }
+    while (len >= 8) {
+        uint64_t w;
+        memcpy(&w, p, 8);
+        c64 = _mm_crc32_u64(c64, w);
+        p += 8;
+        len -= 8;
+    }
+    while (len--) {
+        c64 = _mm_crc32_u8((uint32_t)c64, *p++);
+    }
+    return (uint32_t)c64;
+}
+
+/* Three independent crc32q chains over consecutive thirds of a block, then a
+ * GF(2) shift-combine: the standard way to fill the 3-cycle-latency /
+ * 1-per-cycle-throughput crc32 pipeline.  Two block tiers (8 KiB, 256 B) so
+ * mid-size buffers also run interleaved. */
+static uint32_t g_shift[2][2]; /* [tier][0]=x^(8*2*blk), [tier][1]=x^(8*blk) */
+static const uint32_t g_blk[2] = {8192u, 256u};
+static pthread_once_t g_shift_once = PTHREAD_ONCE_INIT;
+static void init_shift(void)
+{
+    for (int t = 0; t < 2; ++t) {
+        g_shift[t][0] = x8nmodp(2 * (uint64_t)g_blk[t]);
+        g_shift[t][1] = x8nmodp(g_blk[t]);
+    }
+}
+
+__attribute__((target("sse4.2"))) static uint32_t hw3_raw(const uint8_t *p, size_t len, uint32_t c)
+{
+    while (len && ((uintptr_t)p & 7)) {
+        c = _mm_crc32_u8(c, *p++);
+        --len;
+    }
+    for (int t = 0; t < 2; ++t) {
+        const uint32_t blk = g_blk[t];
+        while (len >= 3 * (size_t)blk) {
+            uint64_t c0 = c, c1 = 0, c2 = 0;
+            const uint8_t *p1 = p + blk, *p2 = p + 2 * blk;
+            for (uint32_t i = 0; i < blk; i += 8) {
+                uint64_t w0, w1, w2;
+                memcpy(&w0, p + i, 8);
+                memcpy(&w1, p1 + i, 8);
+                memcpy(&w2, p2 + i, 8);
+                c0 = _mm_crc32_u64(c0, w0);
+                c1 = _mm_crc32_u64(c1, w1);
+                c2 = _mm_crc32_u64(c2, w2);
+            }
+            c = multmodp(g_shift[t][0], (uint32_t)c0) ^ multmodp(g_shift[t][1], (uint32_t)c1) ^
+                (uint32_t)c2;
+            p += 3 * (size_t)blk;
+            len -= 3 * (size_t)blk;
+        }
+    }
+    return hw_raw(p, len, c);
+}
+#endif
+
+uint32_t oracle_crc32c_hw_serial(const void *data, uint32_t len, uint32_t crc)
+{
+    if (len == 0) {
+        return crc;
+    }
+#ifdef ORACLE_HAVE_X86
+    if (oracle_have_sse42()) {
+        return ~hw_raw((const uint8_t *)data, len, ~crc);
+    }
+#endif
+    return oracle_crc32c_sw(data, len, crc);
+}
+
+uint32_t oracle_crc32c_hw(const void *data, uint32_t len, uint32_t crc)
+{
+    if (len == 0) {
+        return crc;
+    }
+#ifdef ORACLE_HAVE_X86
+    if (oracle_have_sse42()) {
+        pthread_once(&g_shift_once, init_shift);
+        return ~hw3_raw((const uint8_t *)data, len, ~crc);
+    }
+#endif
+    return oracle_crc32c_sw(data, len, crc);
+}
+
+/* ------------------------------------------------------------ Blob chain */
+/* bmqp_crc32c.cpp:47-67: empty blob -> crc; otherwise chain per buffer. */
+uint32_t oracle_crc32c_blob(const void *const *bufs, const uint32_t *lens, uint32_t nbuf,
+                            uint32_t crc)
+{
+    for (uint32_t i = 0; i < nbuf; ++i) {
+        crc = oracle_crc32c_bitwise(bufs[i], lens[i], crc);
+    }
+    return crc;
+}
+
+/* ------------------------------------------------------------ batch (CPU) */
+typedef uint32_t (*crc_fn)(const void *, uint32_t, uint32_t);
+
+static crc_fn pick(int variant)
+{
+    switch (variant) {
+    case 0: return oracle_crc32c_hw;
+    case 1: return oracle_crc32c_hw_serial;
+    case 2: return oracle_crc32c_sw;
+    default: return oracle_crc32c_bitwise;
+    }
+}
+
+struct batch_job {
+    const uint8_t *arena;
+    const uint64_t *off;
+    const uint32_t *len;
+    const uint32_t *seed;
+    uint32_t *out;
+    size_t lo, hi;
+    crc_fn fn;
+};
+
+static void *batch_worker(void *arg)
+{
+    struct batch_job *j = (struct batch_job *)arg;
+    for (size_t i = j->lo; i < j->hi; ++i) {
+        j->out[i] = j->fn(j->arena + j->off[i], j->len[i], j->seed ? j->seed[i] : 0u);
+    }
+    return NULL;
+}
+
+/* CRC every message of a batch on `nthreads` host threads, messages split
+ * into contiguous byte-balanced slices (the reference's test5 pattern,
+ * bmqp_crc32c.t.cpp:705-760).  variant: 0 hw 3-way, 1 hw serial, 2 slicing-by-8,
+ * 3 bitwise.  Returns 0. */
+int oracle_crc32c_batch(const uint8_t *arena, const uint64_t *off, const uint32_t *len,
+                        const uint32_t *seed, uint32_t *out, size_t n, int nthreads, int variant)
+{
+    enum { MAXT = 256 };
+    if (nthreads < 1) {
+        nthreads = 1;
+    }
+    if (nthreads > MAXT) {
+        nthreads = MAXT;
+    }
+    pthread_once(&g_tab_once, init_tables);
+    uint64_t total = 0;
+    for (size_t i = 0; i < n; ++i) {
+        total += len[i];
+    }
+    struct batch_job jobs[MAXT];
+    pthread_t th[MAXT];
+    size_t i = 0;
+    uint64_t acc = 0;
+    for (int t = 0; t < nthreads; ++t) {
+        jobs[t].arena = arena;
+        jobs[t].off = off;
+        jobs[t].len = len;
+        jobs[t].seed = seed;
+        jobs[t].out = out;
+        jobs[t].fn = pick(variant);
+        jobs[t].lo = i;
+        uint64_t target = total * (uint64_t)(t + 1) / (uint64_t)nthreads;
+        while (i < n && (acc < target || t == nthreads - 1)) {
+            acc += len[i];
+            ++i;
+        }
+        jobs[t].hi = i;
+    }
+    for (int t = 1; t < nthreads; ++t) {
+        pthread_create(&th[t], NULL, batch_worker, &jobs[t]);
+    }
+    batch_worker(&jobs[0]);
+    for (int t = 1; t < nthreads; ++t) {
+        pthread_join(th[t], NULL);
+    }
+    return 0;
+}
+
+/* Wall-clock seconds for `reps` passes of oracle_crc32c_batch (bench helper). */
+double oracle_time_batch(const uint8_t *arena, const uint64_t *off, const uint32_t *len,
+                         const uint32_t *seed, uint32_t *out, size_t n, int nthreads,
+                         int variant, int reps)
+{
+    struct timespec a, b;
+    clock_gettime(CLOCK_MONOTONIC, &a);
+    for (int r = 0; r < reps; ++r) {
+        oracle_crc32c_batch(arena, off, len, seed, out, n, nthreads, variant);
+    }
+    clock_gettime(CLOCK_MONOTONIC, &b);
+    return (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+}
+
+/* Deterministic synthetic payload bytes shared with the device generator:
+ * byte i of the stream seeded by `seed` is the low byte of
+ * splitmix64(seed * 0x9E3779B97F4A7C15 + (i / 8)) >> (8 * (i % 8)). */
+static uint64_t splitmix64(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+void oracle_fill_payload(uint8_t *dst, uint64_t begin, uint64_t nbytes, uint64_t seed)
+{
+    for (uint64_t i = 0; i < nbytes; ++i) {
+        uint64_t g = begin + i;
+        uint64_t w = splitmix64(seed * 0x9E3779B97F4A7C15ull + (g >> 3));
+        dst[i] = (uint8_t)(w >> (8 * (g & 7)));
+    }
+}

@@ -1,0 +1,38 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu)")
+
+
+def _ensure_built():
+    lib = os.path.join(ROOT, "blazingmq_amd", "lib", "libbmqcrc.so")
+    orc = os.path.join(ROOT, "oracle", "lib", "liboracle_crc32c.so")
+    if not (os.path.exists(lib) and os.path.exists(orc)):
+        import subprocess
+        subprocess.check_call([sys.executable, os.path.join(ROOT, "blazingmq_amd", "build.py")])
+
+
+_ensure_built()
+
+
+@pytest.fixture(scope="session")
+def golden():
+    import json
+    with open(os.path.join(ROOT, "tests", "golden", "crc32c_vectors.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test selected but no GPU is visible")
+    return torch.device("cuda:0")

@@ -1,0 +1,111 @@
+#!/usr/bin/env python3
+"""Extract the reference's CRC32C golden vectors into tests/golden/crc32c_vectors.json.
+
+Run in the build container (where /root/reference exists); the JSON it writes
+is the committed fixture -- the GPU box never reads /root/reference.
+
+Sources (all in /root/reference, read as text):
+  * src/groups/bmq/bmqp/bmqp_crc32c.t.cpp
+      test1 breathing "12345678" -> 0x6087809A              (:311-319)
+      test2 table {line, buffer, crc}                        (:416-434)
+      test4 table {line, buffer, prefixLen, crc}             (:604-622)
+      test7/8 blob "one"+"two"+"three" -> 0xA0EA6901         (:845, :970)
+      test7/8 277-byte sentence + 550 '#' -> 0xD86F726E      (:854-881, :980-1022)
+  * src/applications/bmqstoragetool/integration-tests/data/test.bmq_data
+      (copied verbatim as test.bmq_data) with the journal CRC printed by
+      bmqstoragetool in detail_result.txt:15,53 (3381945770) for the two
+      MESSAGE records at DATA offsets 40 and 64 (payload_dump.txt).
+  * RFC 3720 section B.4 (iSCSI CRC32C test patterns) as external known answers.
+"""
+import json
+import os
+import re
+import shutil
+import sys
+
+REF = "/root/reference"
+T_CPP = os.path.join(REF, "src/groups/bmq/bmqp/bmqp_crc32c.t.cpp")
+DATA_DIR = os.path.join(REF, "src/applications/bmqstoragetool/integration-tests/data")
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def c_unescape(s):
+    return s.encode("latin-1").decode("unicode_escape").encode("latin-1")
+
+
+def table_rows(src, start_marker):
+    i = src.index(start_marker)
+    j = src.index("};", i)
+    return src[i:j]
+
+
+def main():
+    src = open(T_CPP, encoding="latin-1").read()
+    out = {"source": "bmqp_crc32c.t.cpp + bmqstoragetool fixture + RFC3720 B.4"}
+
+    # test2 (first k_DATA table after test2_calculateOnBuffer)
+    t2 = table_rows(src[src.index("static void test2_calculateOnBuffer"):], "k_DATA[] =")
+    vec2 = [(c_unescape(b), int(c, 0))
+            for b, c in re.findall(r'\{L_,\s*"((?:[^"\\]|\\.)*)",\s*(0x[0-9A-Fa-f]+|0)\}', t2)]
+    assert len(vec2) == 19, len(vec2)
+    out["calculate"] = [{"hex": b.hex(), "text": b.decode("latin-1"), "crc": c} for b, c in vec2]
+    out["calculate"].insert(0, {"hex": b"12345678".hex(), "text": "12345678", "crc": 0x6087809A})
+
+    # test4 chained table
+    t4 = table_rows(src[src.index("static void test4_calculateOnBufferWithPreviousCrc"):],
+                    "k_DATA[] =")
+    vec4 = [(c_unescape(b), int(p), int(c, 0)) for b, p, c in re.findall(
+        r'\{L_,\s*"((?:[^"\\]|\\.)*)",\s*(\d+),\s*(0x[0-9A-Fa-f]+|0)\}', t4)]
+    assert len(vec4) == 19, len(vec4)
+    out["chained"] = [{"hex": b.hex(), "prefix_len": p, "crc": c} for b, p, c in vec4]
+
+    # test7 blobs
+    t7 = src[src.index("static void test7_calculateOnBlob"):
+             src.index("static void test8_calculateOnBlobWithPreviousCrc")]
+    assert "0xA0EA6901" in t7 and "0xD86F726E" in t7
+    m = re.search(r'char buf\[\] = ((?:\s*"(?:[^"\\]|\\.)*")+);', t7)
+    sentence = b"".join(c_unescape(x) for x in re.findall(r'"((?:[^"\\]|\\.)*)"', m.group(1)))
+    out["blob"] = [
+        {"buffers_hex": [b"one".hex(), b"two".hex(), b"three".hex()], "crc": 0xA0EA6901},
+        {"buffers_hex": [sentence.hex()], "crc": 0xD86F726E},
+        {"buffers_hex": [], "crc": 0},
+    ]
+    # test8: same content split over two blobs, chained through the CRC
+    t8 = src[src.index("static void test8_calculateOnBlobWithPreviousCrc"):]
+    m1 = re.search(r'char one\[\] = ((?:\s*"(?:[^"\\]|\\.)*")+);', t8)
+    m2 = re.search(r'char two\[\] = ((?:\s*"(?:[^"\\]|\\.)*")+);', t8)
+    one = b"".join(c_unescape(x) for x in re.findall(r'"((?:[^"\\]|\\.)*)"', m1.group(1)))
+    two = b"".join(c_unescape(x) for x in re.findall(r'"((?:[^"\\]|\\.)*)"', m2.group(1)))
+    assert one + two == sentence, (len(one), len(two), len(sentence))
+    out["blob_chained"] = [
+        {"blobs_hex": [[b"one".hex()], [b"two".hex(), b"three".hex()]], "crc": 0xA0EA6901},
+        {"blobs_hex": [[one.hex()], [two.hex()]], "crc": 0xD86F726E},
+        {"blobs_hex": [[]], "seed": 0xA0EA6901, "crc": 0xA0EA6901},
+    ]
+
+    # RFC 3720 B.4
+    out["rfc3720"] = [
+        {"hex": (b"\x00" * 32).hex(), "crc": 0x8A9136AA},
+        {"hex": (b"\xff" * 32).hex(), "crc": 0x62A8AB43},
+        {"hex": bytes(range(32)).hex(), "crc": 0x46DD794E},
+        {"hex": bytes(range(31, -1, -1)).hex(), "crc": 0x113FDB5C},
+    ]
+
+    # on-disk DATA fixture
+    detail = open(os.path.join(DATA_DIR, "detail_result.txt")).read()
+    crcs = [int(x) for x in re.findall(r"Crc32c\s*:\s*(\d+)", detail)]
+    assert crcs == [3381945770, 3381945770], crcs
+    shutil.copyfile(os.path.join(DATA_DIR, "test.bmq_data"), os.path.join(HERE, "test.bmq_data"))
+    out["data_file"] = {
+        "file": "test.bmq_data",
+        "records": [{"record_offset": 40, "header_bytes": 12, "app_data_len": 11, "crc": crcs[0]},
+                    {"record_offset": 64, "header_bytes": 12, "app_data_len": 11, "crc": crcs[1]}],
+    }
+    with open(os.path.join(HERE, "crc32c_vectors.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print("wrote crc32c_vectors.json:", {k: len(v) if isinstance(v, list) else 1
+                                         for k, v in out.items()})
+
+
+if __name__ == "__main__":
+    sys.exit(main())
