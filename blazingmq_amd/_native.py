@@ -32,6 +32,15 @@ class Opts(ctypes.Structure):
                 ("seg_bytes", ctypes.c_uint32)]
 
 
+# One HIP runtime per process: when PyTorch-ROCm is present it ships its own
+# libamdhip64.so (soname libamdhip64.so.7).  Loading torch first lets this
+# library's DT_NEEDED libamdhip64.so.7 bind to that same runtime instead of
+# pulling a second copy from /opt/rocm (two runtimes cannot share a device).
+try:
+    import torch  # noqa: F401
+except ImportError:  # pragma: no cover - torch is optional for the C ABI itself
+    torch = None
+
 if not os.path.exists(LIB_PATH):
     raise ImportError("libbmqcrc.so not built (%s); run `python -c \"import __graft_entry__ as g; "
                       "g.build()\"` first" % LIB_PATH)
