@@ -83,6 +83,19 @@ def cpu_baseline(msg_bytes, seed, seconds):
     }
 
 
+def pmc_traffic(config):
+    """HBM bytes per k_fold launch from the newest committed rocprofv3 PMC
+    summary of this config (profiles/rNN/<config>_summary.json): read =
+    2 x FETCH_SIZE (gfx950 correction) + WRITE_SIZE, per MI355X_MICROARCH.md."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", config + "_summary.json")))
+    if not paths:
+        return None, None
+    with open(paths[-1]) as f:
+        s = json.load(f)
+    return int(s["traffic_bytes_per_launch"]), os.path.relpath(paths[-1], ROOT)
+
+
 def main():
     args = parse()
     import numpy as np
@@ -159,6 +172,7 @@ def main():
         value = gib_all * args.steps / elapsed
         avg_kern_s = (kern_ms / 1e3 / kern_cnt) if kern_cnt else float("nan")
         alg_bytes = total_bytes + 4 * n  # payload read once + CRC written
+        traffic, traffic_src = pmc_traffic(args.config)
         achieved = alg_bytes / avg_kern_s / 1e9
         res = {
             "metric": "device-resident CRC32C GiB/s over batched payloads, 1/2/4/8 MI355X",
@@ -179,7 +193,7 @@ def main():
                        "parallelism": "dp%d (sharded batch, no collective)" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None,
+                         "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "k_fold", "kernel_avg_us": round(avg_kern_s * 1e6, 2),
                          "alg_bytes_per_launch": alg_bytes},
             "parity": {"checked_msgs": int(len(idx)) * world, "mismatches": bad},

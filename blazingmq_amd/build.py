@@ -3,8 +3,8 @@
 * ``blazingmq_amd/lib/libbmqcrc.so`` -- the product: HIP kernels for gfx950
   (hipcc --offload-arch=gfx950) + the C-ABI host code (include/bmqcrc.h).
 * ``oracle/lib/liboracle_crc32c.so`` -- the CPU checker (test infrastructure).
-* ``blazingmq_amd/lib/bmqp_selftest`` -- the C++ drop-in (bmqp::Crc32c) test
-  driver, linked against libbmqcrc.so.
+* ``tests/cpp/bin/bmqp_selftest`` -- the C++ drop-in (bmqp::Crc32c) test
+  driver (test infrastructure), linked against libbmqcrc.so.
 
 hipcc cross-compiles gfx950 code objects without a GPU present.
 """
@@ -64,11 +64,13 @@ def build_product(force=False):
               "-lpthread"])
         for o in objs:
             os.remove(o)
-    selftest = os.path.join(LIB, "bmqp_selftest")
+    selftest = os.path.join(ROOT, "tests", "cpp", "bin", "bmqp_selftest")
     st_src = os.path.join(ROOT, "tests", "cpp", "bmqp_crc32c_selftest.cpp")
     if os.path.exists(st_src) and (force or _stale(selftest, [st_src, target])):
+        os.makedirs(os.path.dirname(selftest), exist_ok=True)
         _run(["g++", "-O2", "-std=c++17", "-I" + os.path.join(ROOT, "include"), st_src,
-              "-o", selftest, "-L" + LIB, "-lbmqcrc", "-Wl,-rpath,$ORIGIN"])
+              "-o", selftest, "-L" + LIB, "-lbmqcrc", "-pthread",
+              "-Wl,-rpath,$ORIGIN/../../../blazingmq_amd/lib"])
     return target
 
 

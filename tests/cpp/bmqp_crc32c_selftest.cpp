@@ -1,0 +1,271 @@
+// bmqp_crc32c_selftest.cpp -- the reference's component test plan for
+// bmqp::Crc32c (/root/reference/src/groups/bmq/bmqp/bmqp_crc32c.t.cpp),
+// re-run against the drop-in include/bmqp_crc32c.h.  Expected values are the
+// reference's own golden constants.
+//
+//   bmqp_selftest            CPU cases 1-5, 7, 8 (+ fuzz property)
+//   bmqp_selftest gpu        additionally calculateBatch on the MI355X
+#include "bmqp_crc32c.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+using BloombergLP::bdlbb::Blob;
+using BloombergLP::bdlbb::BlobBuffer;
+using BloombergLP::bmqp::Crc32c;
+
+static int g_fail = 0;
+#define CHECK_EQ(a, b)                                                                     \
+    do {                                                                                   \
+        unsigned long long a_ = (a), b_ = (b);                                             \
+        if (a_ != b_) {                                                                    \
+            fprintf(stderr, "%s:%d: %s = %#llx != %#llx\n", __FILE__, __LINE__, #a, a_, b_); \
+            ++g_fail;                                                                      \
+        }                                                                                  \
+    } while (0)
+
+struct V {
+    const char* buf;
+    unsigned crc;
+};
+static const V k_DATA[] = {{"", 0},
+                           {"DYB|O", 0},
+                           {"0", 0x629E1AE0},
+                           {"1", 0x90F599E3},
+                           {"2", 0x83A56A17},
+                           {"~", 0x8F9DB87B},
+                           {"22", 0x47B26CF9},
+                           {"fa", 0x8B9F1387},
+                           {"t0-", 0x77E2D1A9},
+                           {"34v}", 0x031AD8A7},
+                           {"shaii", 0xB0638FB5},
+                           {"3jf-_3", 0xE186B745},
+                           {"bonjour", 0x156088D2},
+                           {"vbPHbvtB", 0x12AAFAA6},
+                           {"aoDicgezd", 0xBF5E01C8},
+                           {"123456789", 0xe3069283},
+                           {"gaaXsSP1al", 0xC4E61D23},
+                           {"2Wm9bbNDehd", 0x54A11873},
+                           {"GamS0NJhAl8y", 0x0044AC66}};
+static const size_t k_N = sizeof(k_DATA) / sizeof(*k_DATA);
+
+static void test1_breathing()
+{
+    CHECK_EQ(Crc32c::calculate("12345678", 8), 0x6087809Au);
+    CHECK_EQ(Crc32c::calculate(0, 0), 0u);
+    CHECK_EQ(Crc32c::calculate("12345678", 0), 0u);
+    CHECK_EQ(Crc32c::calculate("12345678", 0, 0x6087809A), 0x6087809Au);
+    const unsigned pre = Crc32c::calculate("12345678", 3);
+    CHECK_EQ(Crc32c::calculate("12345678" + 3, 5, pre), 0x6087809Au);
+}
+
+static void test2_3_buffer_and_misaligned()
+{
+    alignas(16) char scratch[1024];
+    for (size_t i = 0; i < k_N; ++i) {
+        const unsigned len = (unsigned)strlen(k_DATA[i].buf);
+        CHECK_EQ(Crc32c::calculate(k_DATA[i].buf, len), k_DATA[i].crc);
+        for (unsigned mis = 1; mis < 16; ++mis) {
+            memset(scratch, 'X', mis);
+            memcpy(scratch + mis, k_DATA[i].buf, len);
+            CHECK_EQ(Crc32c::calculate(scratch + mis, len), k_DATA[i].crc);
+        }
+    }
+}
+
+static void test4_previous_crc()
+{
+    struct T {
+        const char* buf;
+        unsigned pre;
+        unsigned crc;
+    } d[] = {{"", 0, 0},
+             {"DYB|O--", 5, 0xD1436CCE},
+             {"0sef", 1, 0x50588062},
+             {"13", 1, 0x813E4763},
+             {"2s34faw", 1, 0xED5E0C1C},
+             {"~ahaer", 1, 0x45F10742},
+             {"22aasd", 2, 0x22B28122},
+             {"faghar", 2, 0xD9253928},
+             {"t0-aavk", 3, 0x8A752D3F},
+             {"34v}acv", 4, 0xC36C7D1D},
+             {"shaiig5bg", 5, 0x9E26CF81},
+             {"123456789", 9, 0xe3069283},
+             {"3jf-_3adfg", 6, 0xEDA627B3},
+             {"bonjour421h", 7, 0xD23EF1DF},
+             {"vbPHbvtB45gga", 8, 0xFCC29260},
+             {"aoDicgezd==7h", 9, 0x171D042A},
+             {"gaaXsSP1aldsafad", 10, 0xFD5078EF},
+             {"2Wm9bbNDehd32qf", 11, 0x9F7277C6},
+             {"GamS0NJhAl8yw3th", 12, 0x6033D909}};
+    for (const T& t : d) {
+        const unsigned len = (unsigned)strlen(t.buf);
+        unsigned c = Crc32c::calculate(t.buf, t.pre);
+        c = Crc32c::calculate(t.buf + t.pre, len - t.pre, c);
+        CHECK_EQ(c, t.crc);
+        CHECK_EQ(Crc32c::calculate(t.buf, 0, c), c);
+        CHECK_EQ(Crc32c::calculate(0, 0, c), c);
+    }
+}
+
+static void test5_multithreaded()
+{
+    enum { k_NUM_PAYLOADS = 10000, k_NUM_THREADS = 10 };
+    std::mt19937 rng(5);
+    std::vector<std::string> payloads;
+    for (int i = 0; i < k_NUM_PAYLOADS; ++i) {
+        std::string s(i + 1, '\0');
+        for (auto& ch : s) {
+            ch = (char)rng();
+        }
+        payloads.push_back(s);
+    }
+    std::vector<unsigned> serial;
+    for (auto& p : payloads) {
+        serial.push_back(Crc32c::calculate(p.data(), (unsigned)p.size()));
+    }
+    std::vector<std::vector<unsigned>> res(k_NUM_THREADS);
+    std::vector<std::thread> th;
+    for (int t = 0; t < k_NUM_THREADS; ++t) {
+        th.emplace_back([&, t]() {
+            for (auto& p : payloads) {
+                res[t].push_back(Crc32c::calculate(p.data(), (unsigned)p.size()));
+            }
+        });
+    }
+    for (auto& t : th) {
+        t.join();
+    }
+    for (int t = 0; t < k_NUM_THREADS; ++t) {
+        for (int j = 0; j < k_NUM_PAYLOADS; ++j) {
+            CHECK_EQ(res[t][j], serial[j]);
+        }
+    }
+}
+
+static std::string sentence()
+{
+    std::string s =
+        "This will be put in a blob buffer of typical"
+        " size, and then we will test the crc32c calculation"
+        " (blob version) with only one blob buffer to ensure"
+        " that the logic of the loop works even for one blob"
+        " buffer. Moreover, append some lines bellow to increase"
+        " the size of this buffer.";
+    return s + std::string(550, '#');
+}
+
+static void test7_8_blob()
+{
+    Blob empty;
+    CHECK_EQ(Crc32c::calculate(empty), Crc32c::k_NULL_CRC32C);
+    CHECK_EQ(Crc32c::calculate(empty, 0xA0EA6901), 0xA0EA6901u);
+
+    char one[] = "one", two[] = "two", three[] = "three";
+    Blob b;
+    b.appendDataBuffer(BlobBuffer(one, 3));
+    b.appendDataBuffer(BlobBuffer(two, 3));
+    b.appendDataBuffer(BlobBuffer(three, 5));
+    CHECK_EQ(Crc32c::calculate(b), 0xA0EA6901u);
+
+    Blob b1, b2;
+    b1.appendDataBuffer(BlobBuffer(one, 3));
+    b2.appendDataBuffer(BlobBuffer(two, 3));
+    b2.appendDataBuffer(BlobBuffer(three, 5));
+    CHECK_EQ(Crc32c::calculate(b2, Crc32c::calculate(b1)), 0xA0EA6901u);
+
+    std::string s = sentence();
+    Blob one_buf;
+    one_buf.appendDataBuffer(BlobBuffer(&s[0], (int)s.size()));
+    CHECK_EQ(Crc32c::calculate(one_buf), 0xD86F726Eu);
+
+    // lastDataBufferLength() trims the last buffer only
+    std::string padded = s + "garbage";
+    Blob trimmed;
+    trimmed.appendDataBuffer(BlobBuffer(&padded[0], (int)padded.size()));
+    trimmed.setLastDataBufferLength((int)s.size());
+    CHECK_EQ(Crc32c::calculate(trimmed), 0xD86F726Eu);
+}
+
+static void fuzz_blob_equals_raw()
+{
+    // s_bmqfuzz_bmqp_crc32c.fuzz.cpp:29-55: raw CRC == Blob CRC for any
+    // buffer size in 1..256 and any seed.
+    std::mt19937 rng(77);
+    for (int it = 0; it < 2000; ++it) {
+        const int size = 1 + (int)(rng() % 256);
+        std::string data(size, '\0');
+        for (auto& ch : data) {
+            ch = (char)rng();
+        }
+        const unsigned seed = rng();
+        Blob blob;
+        int pos = 0;
+        while (pos < size) {
+            const int take = 1 + (int)(rng() % (size - pos));
+            blob.appendDataBuffer(BlobBuffer(&data[pos], take));
+            pos += take;
+        }
+        CHECK_EQ(Crc32c::calculate(blob, seed), Crc32c::calculate(data.data(), size, seed));
+    }
+}
+
+static void gpu_batch()
+{
+    if (bmqcrc_device_count() <= 0) {
+        fprintf(stderr, "gpu: no device\n");
+        ++g_fail;
+        return;
+    }
+    std::string arena;
+    std::vector<unsigned long long> off;
+    std::vector<unsigned> len, exp;
+    for (size_t i = 0; i < k_N; ++i) {
+        off.push_back(arena.size());
+        len.push_back((unsigned)strlen(k_DATA[i].buf));
+        exp.push_back(k_DATA[i].crc);
+        arena += k_DATA[i].buf;
+    }
+    std::string s = sentence();
+    off.push_back(arena.size());
+    len.push_back((unsigned)s.size());
+    exp.push_back(0xD86F726E);
+    arena += s;
+    std::vector<unsigned> got(off.size());
+    const int rc = Crc32c::calculateBatch(arena.data(), arena.size(), off.data(), len.data(), 0,
+                                          got.data(), off.size());
+    CHECK_EQ(rc, 0);
+    for (size_t i = 0; i < got.size(); ++i) {
+        CHECK_EQ(got[i], exp[i]);
+    }
+}
+
+int main(int argc, char** argv)
+{
+    test1_breathing();
+    test2_3_buffer_and_misaligned();
+    test4_previous_crc();
+    test5_multithreaded();
+    test7_8_blob();
+    fuzz_blob_equals_raw();
+    if (argc > 1 && strcmp(argv[1], "gpu") == 0) {
+        gpu_batch();
+    } else {
+        // without a GPU the batch path must refuse loudly, never fall back
+        unsigned out = 0;
+        unsigned long long o = 0;
+        unsigned l = 1;
+        const int rc = Crc32c::calculateBatch("x", 1, &o, &l, 0, &out, 1);
+        if (bmqcrc_device_count() == 0) {
+            CHECK_EQ((unsigned)rc, (unsigned)BMQCRC_ENODEV);
+        }
+    }
+    printf("%s: %d failure(s)\n", g_fail ? "FAIL" : "PASS", g_fail);
+    return g_fail ? 1 : 0;
+}

@@ -1,0 +1,47 @@
+"""The C-ABI library loads and exports every entry point include/bmqcrc.h
+declares (no compute on a GPU here)."""
+import ctypes
+import os
+import re
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "blazingmq_amd", "lib", "libbmqcrc.so")
+
+
+def declared():
+    with open(os.path.join(ROOT, "include", "bmqcrc.h")) as f:
+        src = f.read()
+    return sorted(set(re.findall(r"^\w[\w\s\*]*?\b(bmqcrc_\w+)\s*\(", src, re.M)))
+
+
+def test_header_declares_expected_api():
+    names = declared()
+    for n in ("bmqcrc_crc32c", "bmqcrc_crc32c_blob", "bmqcrc_combine", "bmqcrc_crc32c_batch",
+              "bmqcrc_crc32c_batch_multi", "bmqcrc_reserve", "bmqcrc_fill_synthetic",
+              "bmqcrc_kernel_timing", "bmqcrc_device_count", "bmqcrc_last_error",
+              "bmqcrc_version"):
+        assert n in names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(LIB)
+    for n in declared():
+        assert hasattr(lib, n), n
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True).stdout
+    exported = set(l.split()[-1] for l in out.splitlines() if l.strip())
+    assert set(declared()) <= exported
+
+
+def test_library_contains_gfx950_code_object():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", LIB],
+                         capture_output=True, text=True)
+    assert "gfx950" in (out.stdout + out.stderr)
+
+
+def test_version_and_error_string():
+    lib = ctypes.CDLL(LIB)
+    lib.bmqcrc_version.restype = ctypes.c_uint32
+    assert lib.bmqcrc_version() >> 16 == 1
+    lib.bmqcrc_last_error.restype = ctypes.c_char_p
+    assert isinstance(lib.bmqcrc_last_error(), bytes)

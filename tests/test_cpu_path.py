@@ -1,0 +1,93 @@
+"""Host-side product path: scalar/blob CRC through the C ABI, the C++ drop-in
+bmqp::Crc32c, the Python mirror -- all against the oracle and golden vectors.
+(No GPU: these run in the CPU suite.)"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+from blazingmq_amd import Blob, BmqCrcError, Crc32c, device_count
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_scalar_golden(golden):
+    for v in golden["calculate"] + golden["rfc3720"]:
+        assert Crc32c.calculate(bytes.fromhex(v["hex"])) == v["crc"]
+    assert Crc32c.calculate(None, length=0) == 0
+    assert Crc32c.calculate(None, 0x1234, length=0) == 0x1234
+    assert Crc32c.calculate(b"12345678", length=0) == 0
+
+
+def test_scalar_chained(golden):
+    for v in golden["chained"]:
+        b, p = bytes.fromhex(v["hex"]), v["prefix_len"]
+        c = Crc32c.calculate(b[p:], Crc32c.calculate(b[:p]))
+        assert c == v["crc"]
+        assert Crc32c.calculate(b, c, length=0) == c
+
+
+def test_scalar_misaligned_random():
+    rng = np.random.default_rng(21)
+    big = rng.integers(0, 256, size=300000, dtype=np.uint8)
+    for n in list(range(0, 40)) + [191, 192, 193, 1535, 1536, 1537, 12287, 12288, 12289, 100000]:
+        for mis in range(0, 8):
+            buf = big[mis:mis + n]
+            seed = int(rng.integers(0, 2**32))
+            assert Crc32c.calculate(buf, seed) == oracle.crc32c(buf.tobytes(), seed), (n, mis)
+
+
+def test_blob(golden):
+    for v in golden["blob"]:
+        assert Crc32c.calculate_blob(Blob(bytes.fromhex(h) for h in v["buffers_hex"])) == v["crc"]
+    for v in golden["blob_chained"]:
+        c = v.get("seed", 0)
+        for blob in v["blobs_hex"]:
+            c = Crc32c.calculate_blob(Blob(bytes.fromhex(h) for h in blob), c)
+        assert c == v["crc"]
+
+
+def test_blob_fuzz_property():
+    # s_bmqfuzz_bmqp_crc32c.fuzz.cpp: raw CRC == Blob CRC, any split in 1..256, any seed
+    rng = np.random.default_rng(31)
+    for _ in range(300):
+        size = int(rng.integers(1, 257))
+        data = rng.integers(0, 256, size=size, dtype=np.uint8).tobytes()
+        seed = int(rng.integers(0, 2**32))
+        cuts = sorted(set(rng.integers(1, size, size=int(rng.integers(0, 6))).tolist())) if size > 1 else []
+        parts = [data[a:b] for a, b in zip([0] + cuts, cuts + [size])]
+        assert Crc32c.calculate_blob(Blob(parts), seed) == Crc32c.calculate(data, seed)
+
+
+def test_last_data_buffer_length():
+    b = Blob([b"one", b"two", b"threeXYZ"])
+    b.set_last_data_buffer_length(5)
+    assert Crc32c.calculate_blob(b) == 0xA0EA6901
+
+
+def test_combine():
+    rng = np.random.default_rng(41)
+    for _ in range(40):
+        a = rng.integers(0, 256, size=int(rng.integers(0, 5000)), dtype=np.uint8).tobytes()
+        b = rng.integers(0, 256, size=int(rng.integers(0, 5000)), dtype=np.uint8).tobytes()
+        assert Crc32c.combine(Crc32c.calculate(a), Crc32c.calculate(b), len(b)) == \
+            Crc32c.calculate(a + b)
+
+
+def test_cpp_dropin_selftest():
+    exe = os.path.join(ROOT, "tests", "cpp", "bin", "bmqp_selftest")
+    if not os.path.exists(exe):
+        pytest.skip("selftest not built")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "PASS" in r.stdout
+
+
+@pytest.mark.skipif(device_count() > 0, reason="GPU present: batch path is exercised by -m gpu")
+def test_batch_refuses_without_gpu():
+    # the batch path never falls back to the CPU
+    with pytest.raises(BmqCrcError) as e:
+        Crc32c.calculate_batch(np.zeros(64, np.uint8), [0], [64])
+    assert e.value.rc == -19

@@ -1,0 +1,117 @@
+"""CPU model of the device fold algorithm, checked
+against the oracle: sparse-relation word recurrence over a 32-word ring,
+remainder Horner by x^32, x^e move (e mod 2^31-1), seed injection, byte
+masking, segment XOR-combine.  Proves the math the HIP kernel implements."""
+import numpy as np
+import pytest
+
+import oracle
+
+POLY_R = 0x82F63B78
+
+
+def _consts():
+    import importlib.util
+    import os
+    p = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools",
+                     "gen_crc_consts.py")
+    spec = importlib.util.spec_from_file_location("gen", p)
+    g = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(g)
+    taps = [k for k in g.min_poly_of_y() if k < 32]
+    return g, taps
+
+
+G, TAPS = _consts()
+
+
+def mul_y(c):
+    for _ in range(32):
+        c = (c >> 1) ^ (POLY_R if c & 1 else 0)
+    return c
+
+
+def xpow(e):
+    r, sq = 1 << 31, 1 << 30
+    e %= (1 << 31) - 1
+    while e:
+        if e & 1:
+            r = G.mulmod_r(r, sq)
+        sq = G.mulmod_r(sq, sq)
+        e >>= 1
+    return r
+
+
+def fold_stream(words):
+    """raw CRC (zero init, no final xor) of a word stream, len % 32 == 0."""
+    q = [0] * 32
+    nr = len(words) // 32
+    c = 0
+    for r in range(nr):
+        m = words[32 * r:32 * r + 32]
+        if r + 1 < nr:
+            for d in range(32):
+                acc = m[d]
+                for k in TAPS:
+                    acc ^= q[(d + k) & 31]
+                q[d] = acc
+        else:
+            for d in range(32):
+                acc = m[d]
+                for k in TAPS:
+                    if d + k <= 31:
+                        acc ^= q[d + k]
+                c = mul_y(c ^ acc)
+    return c
+
+
+def segment_contrib(arena, S, E, mstart, mend, first, seed):
+    L0 = S & ~127
+    need_end = max(E, S + 4) if first else E
+    nl = (need_end - L0 + 127) // 128
+    stream = bytearray(128 * nl)
+    lo, hi = S - L0, min(E, L0 + 128 * nl) - L0
+    stream[lo:hi] = arena[S:E].tobytes()
+    if first:
+        for b in range(4):
+            stream[lo + b] ^= ((~seed & 0xFFFFFFFF) >> (8 * b)) & 0xFF
+    words = list(np.frombuffer(bytes(stream), dtype="<u4").astype(np.uint64))
+    c = fold_stream([int(w) for w in words])
+    padE = L0 + 128 * nl - E
+    contrib = G.mulmod_r(c, xpow(8 * (mend - E) - 8 * padE))
+    return contrib ^ (0xFFFFFFFF if first else 0)
+
+
+def model_batch(arena, offs, lens, seeds, seg):
+    out = []
+    for off, ln, seed in zip(offs, lens, seeds):
+        if ln == 0:
+            out.append(seed)
+            continue
+        nseg = (ln - 1) // seg + 1
+        b = [off] + [((off + k * seg) & ~127) for k in range(1, nseg)] + [off + ln]
+        acc = 0
+        for k in range(nseg):
+            acc ^= segment_contrib(arena, b[k], b[k + 1], off, off + ln, k == 0, seed)
+        out.append(acc)
+    return out
+
+
+def test_relation_vanishes():
+    acc = 0
+    for k in TAPS + [32]:
+        acc ^= G.ppow(2, 32 * k, G.P_NORMAL)
+    assert acc == 0 and len(TAPS) == 17
+
+
+@pytest.mark.parametrize("seg", [256, 384, 1024])
+def test_model_matches_oracle(seg):
+    rng = np.random.default_rng(seg)
+    arena = rng.integers(0, 256, size=20000, dtype=np.uint8)
+    lens = [0, 1, 2, 3, 4, 5, 31, 127, 128, 129, 300, 1000, 2500]
+    offs = [int(rng.integers(0, arena.size - l)) for l in lens]
+    offs[4] = 126  # seed word crossing a line boundary
+    seeds = [int(rng.integers(0, 2**32)) for _ in lens]
+    got = model_batch(arena, offs, lens, seeds, seg)
+    exp = [oracle.crc32c(arena[o:o + l].tobytes(), s) for o, l, s in zip(offs, lens, seeds)]
+    assert got == exp
