@@ -23,11 +23,42 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 
+# BASELINE.json configs (configs[0] is the reference's CPU-only case).
+#   name: (description, lengths(rank, world) -> (np.uint32 lengths, stream begin), payload seed, scaling)
+ZIPF_N = 4 << 20
+
+
+def _uniform(n, size):
+    def gen(rank, world):
+        import numpy as np
+        return np.full(n, size, dtype=np.uint32), rank * n * size
+    return gen
+
+
+def _zipf(rank, world):
+    """configs[3]: 4M msgs, size = 64*r, r in [1,16384], P(r) ~ r^-1.5 (seed 3),
+    one global batch sharded byte-balanced across the ranks (no collective)."""
+    import numpy as np
+    from blazingmq_amd.shard import rank_slice
+    rng = np.random.default_rng(3)
+    r = np.arange(1, 16385, dtype=np.float64)
+    p = r ** -1.5
+    p /= p.sum()
+    lens = (64 * rng.choice(16384, size=ZIPF_N, p=p) + 64).astype(np.uint32)
+    lo, hi = rank_slice(lens, rank, world)
+    begin = int(lens[:lo].sum(dtype=np.uint64))
+    return lens[lo:hi], begin
+
+
 CONFIGS = {
-    # name: (n_msgs, msg_bytes, seed)  -- BASELINE.json configs[1], [2], [4]
-    "64k_x_64KiB": (65536, 65536, 2),
-    "1M_x_256B": (1 << 20, 256, 1),
-    "16_x_256MiB": (16, 256 << 20, 5),
+    "64k_x_64KiB": ("65,536 msgs x 64 KiB per GPU (configs[2], HBM-bound headline)",
+                    _uniform(65536, 65536), 2, "weak"),
+    "1M_x_256B": ("1,048,576 msgs x 256 B per GPU (configs[1], small-message regime)",
+                  _uniform(1 << 20, 256), 1, "weak"),
+    "zipf_4M": ("4M msgs, Zipf 64 B-1 MiB (r^-1.5), one batch sharded across GPUs (configs[3])",
+                _zipf, 4, "strong"),
+    "16_x_256MiB": ("16 msgs x 256 MiB per GPU (configs[4], multi-chunk fold + combine)",
+                    _uniform(16, 256 << 20), 5, "weak"),
 }
 
 
@@ -36,12 +67,14 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--config", default="64k_x_64KiB", choices=sorted(CONFIGS))
+    p.add_argument("--config", default="64k_x_64KiB", choices=list(CONFIGS))
     p.add_argument("--seg-bytes", type=int, default=0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=2.0,
                    help="approximate wall time of the CPU-baseline sample")
     p.add_argument("--check", type=int, default=256, help="messages checked against the oracle")
+    p.add_argument("--e2e", action="store_true",
+                   help="end-to-end mode: H2D from pinned host + CRC + D2H (for DESIGN.md)")
     return p.parse_args()
 
 
@@ -56,30 +89,35 @@ def cpu_model():
     return platform.processor()
 
 
-def cpu_baseline(msg_bytes, seed, seconds):
+def cpu_baseline(lens_np, seed, seconds):
     """Reference-equivalent CPU CRC32C (oracle, SSE4.2 3-way; BDE 4.39 is not
-    available offline) on a bounded sample of the same synthetic workload."""
+    available offline) on a bounded sample (first ~256 MiB of messages) of the
+    same synthetic workload, on up to 16 host threads (this GPU's CPU share)."""
     import numpy as np
     import oracle
     threads = min(os.cpu_count() or 1, 16)
-    n = max(1, (256 << 20) // msg_bytes)  # 256 MiB sample of the same stream
-    arena = oracle.fill_payload(0, n * msg_bytes, seed)
-    offs = np.arange(n, dtype=np.uint64) * msg_bytes
-    lens = np.full(n, msg_bytes, dtype=np.uint32)
+    csum = np.cumsum(lens_np, dtype=np.uint64)
+    n = max(1, int(np.searchsorted(csum, 256 << 20, side="right")))
+    lens = np.ascontiguousarray(lens_np[:n])
+    offs = np.zeros(n, dtype=np.uint64)
+    if n > 1:
+        offs[1:] = csum[:n - 1]
+    nbytes = int(lens.sum(dtype=np.uint64))
+    arena = oracle.fill_payload(0, nbytes, seed)
     t1, _ = oracle.time_batch(arena, offs, lens, 1, "hw", 1)          # single thread
     t, _ = oracle.time_batch(arena, offs, lens, threads, "hw", 1)      # calibrate
     reps = max(1, int(seconds / max(t, 1e-6)))
     t, _ = oracle.time_batch(arena, offs, lens, threads, "hw", reps)
-    gib = n * msg_bytes / 2**30
+    gib = nbytes / 2**30
     return {
         "value": round(gib * reps / t, 3),
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
-        "sample": "%d msgs x %d B (%.0f MiB) of the same synthetic stream, %d passes; "
-                  "SSE4.2 crc32q 3-way interleaved (bdlde::Crc32c default analogue); "
-                  "single-thread %.2f GiB/s; host %s, nproc %d"
-                  % (n, msg_bytes, gib * 1024, reps, gib / t1, cpu_model(), os.cpu_count()),
+        "sample": "first %d msgs (%.0f MiB) of the same synthetic batch, %d passes on %d "
+                  "threads; SSE4.2 crc32q 3-way interleaved (bdlde::Crc32c default analogue, "
+                  "oracle/crc32c_oracle.c); single-thread %.2f GiB/s; host %s, nproc %d"
+                  % (n, gib * 1024, reps, threads, gib / t1, cpu_model(), os.cpu_count()),
     }
 
 
@@ -113,18 +151,26 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    n, msg_bytes, seed = CONFIGS[args.config]
-    total_bytes = n * msg_bytes
-    # rank r owns messages [r*n, (r+1)*n) of the global batch: its slice of the
-    # synthetic stream starts at byte r*n*msg_bytes.
-    arena = torch.empty(total_bytes, dtype=torch.uint8, device=dev)
+    desc, gen, seed, scaling = CONFIGS[args.config]
+    lens_np, begin = gen(rank, world)
+    n = int(lens_np.size)
+    offs_np = np.zeros(n, dtype=np.int64)
+    if n > 1:
+        np.cumsum(lens_np[:-1], dtype=np.int64, out=offs_np[1:])
+    total_bytes = int(lens_np.sum(dtype=np.uint64))
+    # This rank's messages are bytes [begin, begin + total) of synthetic stream
+    # `seed`, generated in HBM; offsets are relative to the rank's arena.
+    arena = torch.empty(max(total_bytes, 8), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
-    # device-side fill of the rank's slice (begin offset via seed stream index)
-    _fill_slice(bmq, arena, seed, rank * total_bytes)
-    offsets = torch.arange(n, dtype=torch.int64, device=dev) * msg_bytes
-    lengths = torch.full((n,), msg_bytes, dtype=torch.int32, device=dev)
+    _fill_slice(bmq, arena, seed, begin)
+    offsets = torch.from_numpy(offs_np).to(dev)
+    lengths = torch.from_numpy(lens_np.view(np.int32)).to(dev)
     out = torch.empty(n, dtype=torch.int32, device=dev)
     torch.cuda.synchronize(dev)
+
+    if args.e2e:
+        return e2e(args, dev, stream, arena, offs_np, lens_np, total_bytes, world, rank, dist,
+                   desc)
 
     def step(timed):
         Crc32c.calculate_batch(arena, offsets, lengths, None, out, seg_bytes=args.seg_bytes,
@@ -147,33 +193,44 @@ def main():
         dist.barrier()
     elapsed = t1 - t0
     kern_ms, kern_cnt = bmq.kernel_timing(local, stream)
+    bytes_all = total_bytes
+    kern_max = kern_ms / max(kern_cnt, 1)
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64)
+        tt = torch.tensor([elapsed, kern_max], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+        elapsed, kern_max = float(tt[0]), float(tt[1])
+        bt = torch.tensor([total_bytes, n], dtype=torch.int64)
+        dist.all_reduce(bt)
+        bytes_all, n_all = int(bt[0]), int(bt[1])
+    else:
+        n_all = n
 
     # parity spot check against the CPU oracle (sampled messages)
     import oracle
     got = out.cpu().numpy().view(np.uint32)
     rng = np.random.default_rng(rank)
     idx = np.unique(np.concatenate([[0, n - 1], rng.integers(0, n, size=max(0, args.check - 2))]))
-    bad = 0
+    budget = 256 << 20  # bytes of payload regenerated on the host for checking
+    bad, checked = 0, 0
     for i in idx:
-        begin = rank * total_bytes + int(i) * msg_bytes
-        exp = oracle.crc32c(oracle.fill_payload(begin, msg_bytes, seed), 0, "hw")
+        ln = int(lens_np[i])
+        if checked and ln > budget:
+            continue
+        budget -= ln
+        exp = oracle.crc32c(oracle.fill_payload(begin + int(offs_np[i]), ln, seed), 0, "hw")
         bad += int(got[i] != exp)
+        checked += 1
     if world > 1:
-        bt = torch.tensor([bad], dtype=torch.int64)
+        bt = torch.tensor([bad, checked], dtype=torch.int64)
         dist.all_reduce(bt)
-        bad = int(bt.item())
+        bad, checked = int(bt[0]), int(bt[1])
 
     if rank == 0:
-        gib_all = world * total_bytes / 2**30
-        value = gib_all * args.steps / elapsed
-        avg_kern_s = (kern_ms / 1e3 / kern_cnt) if kern_cnt else float("nan")
-        alg_bytes = total_bytes + 4 * n  # payload read once + CRC written
-        traffic, traffic_src = pmc_traffic(args.config)
+        value = bytes_all / 2**30 * args.steps / elapsed
+        avg_kern_s = kern_max / 1e3
+        alg_bytes = total_bytes + 4 * n  # this GPU's payload read once + CRCs written
         achieved = alg_bytes / avg_kern_s / 1e9
+        traffic, traffic_src = pmc_traffic(args.config)
         res = {
             "metric": "device-resident CRC32C GiB/s over batched payloads, 1/2/4/8 MI355X",
             "value": round(value, 2),
@@ -183,27 +240,73 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "u32",
-            "data": "synthetic (splitmix64 random bytes, generated in HBM)",
-            "config": {"workload": "%s: %d msgs x %d B per GPU (BASELINE configs)"
-                       % (args.config, n, msg_bytes), "n_msgs_per_gpu": n,
-                       "msg_bytes": msg_bytes, "seg_bytes": args.seg_bytes or 16384,
+            "data": "synthetic (splitmix64 random payload bytes generated in HBM)",
+            "config": {"workload": args.config + ": " + desc,
+                       "n_msgs_total": n_all, "payload_bytes_total": bytes_all,
+                       "seg_bytes": args.seg_bytes or 16384,
                        "parallelism": "dp%d (sharded batch, no collective)" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "k_fold", "kernel_avg_us": round(avg_kern_s * 1e6, 2),
                          "alg_bytes_per_launch": alg_bytes},
-            "parity": {"checked_msgs": int(len(idx)) * world, "mismatches": bad},
+            "parity": {"checked_msgs": checked, "mismatches": bad},
         }
         if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(msg_bytes, seed, args.cpu_seconds)
+            res["cpu_baseline"] = cpu_baseline(lens_np, seed, args.cpu_seconds)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
     return 1 if bad else 0
+
+
+def e2e(args, dev, stream, arena_dev, offs_np, lens_np, total_bytes, world, rank, dist, desc):
+    """End-to-end: payload starts in pinned host memory (broker blob buffers),
+    H2D copy + batch CRC + D2H of the CRCs, timed per step.  Reported in
+    DESIGN.md, never as the bench `value`."""
+    import torch
+    from blazingmq_amd import Crc32c
+    n = lens_np.size
+    host = torch.empty(arena_dev.numel(), dtype=torch.uint8, pin_memory=True)
+    host.copy_(arena_dev)
+    offsets = torch.from_numpy(offs_np).to(dev)
+    lengths = torch.from_numpy(lens_np.view("int32")).to(dev)
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    out_host = torch.empty(n, dtype=torch.int32, pin_memory=True)
+
+    def step():
+        arena_dev.copy_(host, non_blocking=True)
+        Crc32c.calculate_batch(arena_dev, offsets, lengths, None, out, seg_bytes=args.seg_bytes,
+                               stream=stream, sync=False)
+        out_host.copy_(out, non_blocking=True)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    # H2D alone
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        arena_dev.copy_(host, non_blocking=True)
+    torch.cuda.synchronize(dev)
+    h2d = time.perf_counter() - t0
+    if rank == 0:
+        print(json.dumps({
+            "metric": "end-to-end CRC32C GiB/s incl. H2D payload + D2H CRCs (pinned host)",
+            "value": round(total_bytes * world / 2**30 * args.steps / el, 2), "unit": "GiB/s",
+            "n_gpus": world, "steps": args.steps, "config": args.config + ": " + desc,
+            "h2d_only_GiBps": round(total_bytes / 2**30 * args.steps / h2d, 2),
+            "ms_per_step": round(1e3 * el / args.steps, 3)}), flush=True)
+    return 0
 
 
 def _fill_slice(bmq, arena, seed, begin):

@@ -12,6 +12,7 @@ constexpr int kWavesPerBlock = 4;
 constexpr int kSlots = 2;                                  // LDS ring depth per wave
 constexpr int kSlotBytes = kWaveLanes * kLine;             // 8 KiB per round per wave
 constexpr int kLdsBytes = kWavesPerBlock * kSlots * kSlotBytes;  // 64 KiB per block
+constexpr int kTabBytes = 8 * 256 * 4;  // remainder-reduction slicing tables (LDS)
 constexpr uint32_t kDefaultSegBytes = 16384;
 constexpr int kPlanBlock = 1024;
 

@@ -40,6 +40,8 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const u32x4 lds_cu4;
 
 __constant__ uint32_t c_x2col[31][32] = BMQCRC_X2COL;
+__constant__ uint32_t c_xneg8[136] = BMQCRC_XNEG8;
+__constant__ uint32_t c_ty[8][256] = BMQCRC_TY;
 
 // ------------------------------------------------------------ GF(2) helpers
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
@@ -88,6 +90,18 @@ __device__ uint32_t mul_xpow(uint32_t v, uint32_t e)
         v = bit ? (a0 ^ a1) : v;
     }
     return v;
+}
+
+// v * w mod P (reflected), both variable: 32 shift-and-add steps, 160 VALU.
+__device__ __forceinline__ uint32_t gmul(uint32_t v, uint32_t w)
+{
+    uint32_t acc = 0;
+#pragma unroll
+    for (int t = 31; t >= 0; --t) {  // bit t of v <-> x^(31-t); w tracks w * x^(31-t)
+        acc = xand(acc, bitmask(v, t), w);
+        w = xand(w >> 1, bitmask(w, 0), 0x82F63B78u);
+    }
+    return acc;
 }
 
 __device__ __forceinline__ uint32_t mersenne31(uint64_t x)
@@ -148,12 +162,22 @@ __device__ __forceinline__ void fold_round(uint32_t (&q)[32], const uint32_t (&m
     }
 }
 
-// Final round: the last 32 words are the remainder coefficients.  Taps that
-// would reach this round's (non-existent) quotient words are dropped; the
-// remainder is then reduced by Horner with x^32:  raw = sum R_d y^(32-d).
-__device__ __forceinline__ uint32_t tail_round(const uint32_t (&q)[32], const uint32_t (&m)[32])
+// Final round: the last 32 words are the remainder coefficients R_d of the
+// stream modulo m(y).  Taps that would reach this round's (non-existent)
+// quotient words are dropped.  The remainder is reduced once per segment,
+// raw = sum R_d y^(32-d), by Horner two words per step with slicing tables in
+// LDS (tab[k][b], k<4: (b<<8k)*y, k>=4: (b<<8(k-4))*y^2):
+//   c <- (c ^ R_d) * y^2  ^  R_{d+1} * y
+__device__ __forceinline__ uint32_t tab_lookup(uint32_t tab_lds, int k, uint32_t b)
 {
-    uint32_t c = 0;
+    return *(const __attribute__((address_space(3))) uint32_t*)(uintptr_t)(tab_lds + k * 1024u +
+                                                                           b * 4u);
+}
+
+__device__ __forceinline__ uint32_t tail_round(const uint32_t (&q)[32], const uint32_t (&m)[32],
+                                               uint32_t tab_lds)
+{
+    uint32_t R[32];
 #pragma unroll
     for (int d = 0; d < 32; ++d) {
         uint32_t acc = m[d];
@@ -174,7 +198,20 @@ __device__ __forceinline__ uint32_t tail_round(const uint32_t (&q)[32], const ui
         if (have) {
             acc ^= pend;
         }
-        c = mul_y(c ^ acc);
+        R[d] = acc;
+    }
+    uint32_t c = 0;
+#pragma unroll
+    for (int d = 0; d < 32; d += 2) {
+        const uint32_t v = c ^ R[d];
+        const uint32_t w = R[d + 1];
+        const uint32_t hi = xor3(tab_lookup(tab_lds, 4, v & 0xffu),
+                                 tab_lookup(tab_lds, 5, (v >> 8) & 0xffu),
+                                 tab_lookup(tab_lds, 6, (v >> 16) & 0xffu));
+        const uint32_t lo = xor3(tab_lookup(tab_lds, 0, w & 0xffu),
+                                 tab_lookup(tab_lds, 1, (w >> 8) & 0xffu),
+                                 tab_lookup(tab_lds, 2, (w >> 16) & 0xffu));
+        c = xor3(hi, lo, tab_lookup(tab_lds, 7, v >> 24) ^ tab_lookup(tab_lds, 3, w >> 24));
     }
     return c;
 }
@@ -268,11 +305,19 @@ __device__ uint32_t find_msg(const uint32_t* seg_first, uint64_t n, uint32_t g)
 
 __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kTabBytes + kLdsBytes];
 
     const int lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t wave_lds = (uint32_t)(uintptr_t)(lds_u8*)lds + wave * (kSlots * kSlotBytes);
+    const uint32_t tab_lds = (uint32_t)(uintptr_t)(lds_u8*)lds;
+    const uint32_t wave_lds = tab_lds + kTabBytes + wave * (kSlots * kSlotBytes);
+
+    // remainder-reduction tables -> LDS (8 KiB, once per block; no DMA in flight yet)
+    for (uint32_t t = threadIdx.x; t < 8u * 256u; t += blockDim.x) {
+        *(__attribute__((address_space(3))) uint32_t*)(uintptr_t)(tab_lds + 4u * t) =
+            c_ty[t >> 8][t & 255u];
+    }
+    __syncthreads();
 
     const uint32_t total = a.ctrl->total_segs;
     const uint32_t identity = a.ctrl->identity;
@@ -303,7 +348,6 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         const uint64_t S = (k == 0) ? mstart : ((mstart + (uint64_t)k * SEG) & ~127ull);
         const uint64_t E = (k + 1 == nseg) ? mend : ((mstart + (uint64_t)(k + 1) * SEG) & ~127ull);
         const bool first = valid && k == 0;
-        const bool single = valid && nseg == 1;
         const uint64_t L0 = S & ~127ull;
         const uint64_t need_end = (first && E < S + 4) ? S + 4 : E;
         const uint32_t nl = valid ? (uint32_t)((need_end - L0 + 127u) >> 7) : 0u;
@@ -368,27 +412,47 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
             if (r + 1 < nl) {
                 fold_round(q, m);
             } else if (r + 1 == nl) {
-                crc = tail_round(q, m);
+                crc = tail_round(q, m, tab_lds);
             }
         }
 
         // ------------------------------------------------ move + combine
+        // raw(stream) = raw(segment) * x^(8 padE): un-shift the zero padding
+        // (table x^-8p + one 160-VALU multiply), then move the segment to the
+        // message end with x^(8 after) (sparse exponent: bits no lane needs are
+        // skipped wave-uniformly).
+        uint32_t contrib = 0;
         if (valid) {
-            const uint64_t stream_end = L0 + ((uint64_t)nl << 7);
-            const uint64_t padE = stream_end - E;
-            const uint64_t after = mend - E;
-            const uint32_t e = mersenne31(8ull * after + 8ull * 0x7fffffffull - 8ull * padE);
-            uint32_t contrib = mul_xpow(crc, e);
-            if (first) {
-                contrib ^= 0xffffffffu;
+            const uint32_t padE = (uint32_t)(L0 + ((uint64_t)nl << 7) - E);
+            contrib = gmul(crc, c_xneg8[padE]);
+        }
+        const uint32_t e_after = valid ? mersenne31(8ull * (mend - E)) : 0u;
+        contrib = mul_xpow(contrib, e_after);
+        if (first) {
+            contrib ^= 0xffffffffu;
+        }
+        // XOR-reduce the runs of lanes that hold segments of the same message
+        // (segments of a message are consecutive), then one store or atomic
+        // per run: the run head owns the result.
+        const uint32_t key = valid ? msg : 0xffffffffu;
+        uint32_t haslast = (valid && k + 1 == nseg) ? 1u : 0u;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t ov = (uint32_t)__shfl_down((int)contrib, o);
+            const uint32_t okey = (uint32_t)__shfl_down((int)key, o);
+            const uint32_t ol = (uint32_t)__shfl_down((int)haslast, o);
+            if (lane + o < 64 && okey == key) {
+                contrib ^= ov;
+                haslast |= ol;
             }
-            if (single) {
-                a.out[msg] = contrib;
+        }
+        const uint32_t pkey = (uint32_t)__shfl_up((int)key, 1);
+        if (valid && (lane == 0 || pkey != key)) {
+            if (k == 0 && haslast) {
+                a.out[msg] = contrib;  // whole message inside this wave
             } else {
                 atomicXor(&a.out[msg], contrib);
             }
-        } else {
-            (void)mul_xpow(0u, 0u);  // keep the wave's ballots converged
         }
     }
 }

@@ -168,3 +168,88 @@ def test_fill_matches_oracle_stream(cuda):
     fill_synthetic(t, 42)
     torch.cuda.synchronize()
     assert np.array_equal(t.cpu().numpy(), oracle.fill_payload(0, t.numel(), 42))
+
+
+# ----------------------------------------------------------------------------
+# BASELINE.json configurations at full size
+# ----------------------------------------------------------------------------
+def _device_batch_from_stream(cuda, lens, seed, seg_bytes=0):
+    import torch
+    from blazingmq_amd import fill_synthetic
+    lens = np.asarray(lens, dtype=np.uint32)
+    offs = np.zeros(lens.size, dtype=np.int64)
+    np.cumsum(lens[:-1], dtype=np.int64, out=offs[1:])
+    total = int(lens.sum(dtype=np.uint64))
+    arena = torch.empty(total + 8, dtype=torch.uint8, device=cuda)
+    fill_synthetic(arena, seed)
+    o = torch.from_numpy(offs).to(cuda)
+    ln = torch.from_numpy(lens.view(np.int32)).to(cuda)
+    out = Crc32c.calculate_batch(arena, o, ln, seg_bytes=seg_bytes)
+    return arena, offs, lens, out.cpu().numpy().view(np.uint32)
+
+
+def _oracle_all(arena_t, offs, lens):
+    host = arena_t.cpu().numpy()
+    return oracle.batch(host, offs.astype(np.uint64), lens, nthreads=16)
+
+
+def test_config_1M_x_256B_full(cuda):
+    arena, offs, lens, got = _device_batch_from_stream(cuda, np.full(1 << 20, 256), 1)
+    assert np.array_equal(got, _oracle_all(arena, offs, lens))
+
+
+def test_config_64k_x_64KiB_sampled_and_seg_invariant(cuda):
+    arena, offs, lens, got = _device_batch_from_stream(cuda, np.full(65536, 65536), 2)
+    rng = np.random.default_rng(0)
+    for i in np.unique(np.concatenate([[0, 65535], rng.integers(0, 65536, 1022)])):
+        exp = oracle.crc32c(oracle.fill_payload(int(offs[i]), 65536, 2), 0, "hw")
+        assert got[i] == exp, i
+    # size-independent property: the segment size must not change any result
+    import torch
+    o = torch.from_numpy(offs).to(cuda)
+    ln = torch.from_numpy(lens.view(np.int32)).to(cuda)
+    for seg in (1024, 4096, 65536):
+        alt = Crc32c.calculate_batch(arena, o, ln, seg_bytes=seg).cpu().numpy().view(np.uint32)
+        assert np.array_equal(alt, got), seg
+
+
+def test_config_16_x_256MiB_full(cuda):
+    arena, offs, lens, got = _device_batch_from_stream(cuda, np.full(16, 256 << 20), 5)
+    assert np.array_equal(got, _oracle_all(arena, offs, lens))
+    # chaining property: CRC of the 4 GiB concatenation equals combining the
+    # 16 message CRCs (here: one 2^32-1-byte-capped message cannot hold it,
+    # so check pairs: crc(m0||m1) == combine(crc m0, crc m1, len m1))
+    import torch
+    o = torch.tensor([0], dtype=torch.int64, device=cuda)
+    ln = torch.tensor([np.uint32(512 << 20).view(np.int32)], dtype=torch.int32, device=cuda)
+    pair = int(Crc32c.calculate_batch(arena, o, ln).cpu().numpy().view(np.uint32)[0])
+    assert pair == Crc32c.combine(int(got[0]), int(got[1]), 256 << 20)
+
+
+def test_config_zipf_full(cuda):
+    rng = np.random.default_rng(3)
+    r = np.arange(1, 16385, dtype=np.float64)
+    p = r ** -1.5
+    p /= p.sum()
+    lens = (64 * rng.choice(16384, size=4 << 20, p=p) + 64).astype(np.uint32)
+    arena, offs, lens, got = _device_batch_from_stream(cuda, lens, 4)
+    assert np.array_equal(got, _oracle_all(arena, offs, lens))
+
+
+def test_multi_device_host_api(cuda):
+    from blazingmq_amd import calculate_batch_multi, device_count
+    rng = np.random.default_rng(17)
+    arena = rng.integers(0, 256, size=8 << 20, dtype=np.uint8)
+    lens = rng.integers(0, 70000, size=400)
+    offs = np.array([rng.integers(0, arena.size - l + 1) for l in lens], dtype=np.uint64)
+    devs = list(range(device_count())) * 2  # same device twice = two shards/streams
+    got = calculate_batch_multi(arena, offs, lens, devices=devs)
+    assert np.array_equal(got, oracle.batch(arena, offs, lens, nthreads=8))
+
+
+def test_cpp_dropin_gpu_batch(cuda):
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(__file__), "cpp", "bin", "bmqp_selftest")
+    r = subprocess.run([exe, "gpu"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "PASS" in r.stdout, r.stdout + r.stderr
