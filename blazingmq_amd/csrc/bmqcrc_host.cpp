@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -211,6 +212,11 @@ int batch_one(int dev, void* user_stream, uint32_t flags, uint32_t seg, const vo
     memset(&a, 0, sizeof(a));
     a.n = n;
     a.seg_bytes = seg;
+    static const uint32_t tune = [] {
+        const char* e = getenv("BMQCRC_TUNE");  // experiment knob, see BatchArgs::tune
+        return e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
+    }();
+    a.tune = tune;
     if ((rc = plan_ws(w, n, arena_bytes, seg, &a))) {
         return rc;
     }

@@ -40,6 +40,9 @@ struct BatchArgs {
     uint32_t seg_bytes;
     uint32_t nblocks;          // planner blocks = ceil(n / kPlanBlock)
     uint64_t max_segs;
+    uint32_t tune;             // experiment knobs (BMQCRC_TUNE env): bit0 disables nt LDS-DMA
+                               // loads, bit1 selects a 1-block/CU grid
+    uint32_t pad;
 };
 
 }  // namespace bmqcrc

@@ -245,6 +245,36 @@ __device__ __forceinline__ void mask_round(uint32_t (&m)[32], int sR, int eR, bo
 
 // Issue one round of LDS-DMA: 8 x global_load_lds_dwordx4 (8 x 1 KiB), each
 // covering 8 segments x one full 128-byte line.  M0 = LDS destination.
+#define BMQCRC_DMA_ASM(CP)                                                                    \
+    "s_waitcnt lgkmcnt(0)\n\t"                                                              \
+    "s_mov_b32 %0, m0\n\t"                                                                  \
+    "s_mov_b32 m0, %1\n\t"                                                                  \
+    "s_nop 0\n\t"                                                                           \
+    "global_load_lds_dwordx4 %2, off" CP "\n\t"                                             \
+    "s_add_u32 m0, m0, 0x400\n\t"                                                           \
+    "s_nop 0\n\t"                                                                           \
+    "global_load_lds_dwordx4 %3, off" CP "\n\t"                                             \
+    "s_add_u32 m0, m0, 0x400\n\t"                                                           \
+    "s_nop 0\n\t"                                                                           \
+    "global_load_lds_dwordx4 %4, off" CP "\n\t"                                             \
+    "s_add_u32 m0, m0, 0x400\n\t"                                                           \
+    "s_nop 0\n\t"                                                                           \
+    "global_load_lds_dwordx4 %5, off" CP "\n\t"                                             \
+    "s_add_u32 m0, m0, 0x400\n\t"                                                           \
+    "s_nop 0\n\t"                                                                           \
+    "global_load_lds_dwordx4 %6, off" CP "\n\t"                                             \
+    "s_add_u32 m0, m0, 0x400\n\t"                                                           \
+    "s_nop 0\n\t"                                                                           \
+    "global_load_lds_dwordx4 %7, off" CP "\n\t"                                             \
+    "s_add_u32 m0, m0, 0x400\n\t"                                                           \
+    "s_nop 0\n\t"                                                                           \
+    "global_load_lds_dwordx4 %8, off" CP "\n\t"                                             \
+    "s_add_u32 m0, m0, 0x400\n\t"                                                           \
+    "s_nop 0\n\t"                                                                           \
+    "global_load_lds_dwordx4 %9, off" CP "\n\t"                                             \
+    "s_mov_b32 m0, %0\n\t"
+
+template <bool NT>
 __device__ __forceinline__ void dma_round(uint32_t lds_dst, const uint64_t (&dbase)[8],
                                           const uint32_t (&dlim)[8], uint32_t r)
 {
@@ -254,34 +284,15 @@ __device__ __forceinline__ void dma_round(uint32_t lds_dst, const uint64_t (&dba
         s[i] = dbase[i] + ((uint64_t)min(r, dlim[i]) << 7);
     }
     uint32_t keep;
-    asm volatile(
-        "s_waitcnt lgkmcnt(0)\n\t"
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %1\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %2, off\n\t"
-        "s_add_u32 m0, m0, 0x400\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %3, off\n\t"
-        "s_add_u32 m0, m0, 0x400\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %4, off\n\t"
-        "s_add_u32 m0, m0, 0x400\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %5, off\n\t"
-        "s_add_u32 m0, m0, 0x400\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %6, off\n\t"
-        "s_add_u32 m0, m0, 0x400\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %7, off\n\t"
-        "s_add_u32 m0, m0, 0x400\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %8, off\n\t"
-        "s_add_u32 m0, m0, 0x400\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %9, off\n\t"
-        "s_mov_b32 m0, %0\n\t"
+    if (NT) {
+        asm volatile(BMQCRC_DMA_ASM(" nt")
+        : "=&s"(keep)
+        : "s"(lds_dst), "v"(s[0]), "v"(s[1]), "v"(s[2]), "v"(s[3]), "v"(s[4]), "v"(s[5]),
+          "v"(s[6]), "v"(s[7])
+        : "memory", "scc");
+        return;
+    }
+    asm volatile(BMQCRC_DMA_ASM("")
         : "=&s"(keep)
         : "s"(lds_dst), "v"(s[0]), "v"(s[1]), "v"(s[2]), "v"(s[3]), "v"(s[4]), "v"(s[5]),
           "v"(s[6]), "v"(s[7])
@@ -303,6 +314,7 @@ __device__ uint32_t find_msg(const uint32_t* seg_first, uint64_t n, uint32_t g)
     return (uint32_t)lo;
 }
 
+template <bool NT>
 __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kTabBytes + kLdsBytes];
@@ -378,9 +390,9 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         const uint32_t c0 = ~seed;
         const uint64_t inj_end = first ? S + 4 : S;
 
-        dma_round(wave_lds, dbase, dlim, 0);
+        dma_round<NT>(wave_lds, dbase, dlim, 0);
         if (R > 1) {
-            dma_round(wave_lds + kSlotBytes, dbase, dlim, 1);
+            dma_round<NT>(wave_lds + kSlotBytes, dbase, dlim, 1);
         }
         for (uint32_t r = 0; r < R; ++r) {
             const uint32_t slot = wave_lds + (r & 1u) * kSlotBytes;
@@ -399,7 +411,7 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
                 m[4 * kk + 3] = v.w;
             }
             if (r + 2 < R) {
-                dma_round(slot, dbase, dlim, r + 2);
+                dma_round<NT>(slot, dbase, dlim, r + 2);
             }
             const uint64_t p0 = L0 + ((uint64_t)r << 7);
             if (r < nl && (p0 < inj_end || p0 + 128u > E)) {
@@ -626,7 +638,7 @@ extern "C" int bmqcrc_launch_batch(const BatchArgs* a, void* stream, int num_cus
     hipLaunchKernelGGL(k_plan_emit, dim3((unsigned)emit_blocks), dim3(256), 0, s, *a);
     const uint64_t max_groups = (a->max_segs + 63) / 64;
     uint64_t grid = (max_groups + kWavesPerBlock - 1) / kWavesPerBlock;
-    const uint64_t cap = (uint64_t)(num_cus > 0 ? num_cus : 256) * 2;
+    const uint64_t cap = (uint64_t)(num_cus > 0 ? num_cus : 256) * (a->tune & 2u ? 1u : 2u);
     if (grid > cap) {
         grid = cap;
     }
@@ -636,7 +648,12 @@ extern "C" int bmqcrc_launch_batch(const BatchArgs* a, void* stream, int num_cus
     if (ev_start) {
         (void)hipEventRecord((hipEvent_t)ev_start, s);
     }
-    hipLaunchKernelGGL(k_fold, dim3((unsigned)grid), dim3(kWavesPerBlock * 64), 0, s, *a);
+    if (!(a->tune & 1u)) {  // default: non-temporal LDS-DMA (once-read stream)
+        hipLaunchKernelGGL(k_fold<true>, dim3((unsigned)grid), dim3(kWavesPerBlock * 64), 0, s, *a);
+    } else {
+        hipLaunchKernelGGL(k_fold<false>, dim3((unsigned)grid), dim3(kWavesPerBlock * 64), 0, s,
+                           *a);
+    }
     if (ev_stop) {
         (void)hipEventRecord((hipEvent_t)ev_stop, s);
     }
