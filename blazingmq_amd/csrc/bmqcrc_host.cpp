@@ -51,11 +51,14 @@ int fail(int rc, const std::string& msg)
 struct DevBuf {
     void* p = nullptr;
     uint64_t bytes = 0;
+    bool fresh = false;  // set when ensure() (re)allocated
     int ensure(uint64_t want)
     {
+        fresh = false;
         if (want <= bytes) {
             return 0;
         }
+        fresh = true;
         if (p) {
             (void)hipFree(p);
             p = nullptr;
@@ -77,7 +80,7 @@ struct DevBuf {
 // Planner + staging scratch for one (device, stream).
 struct Workspace {
     std::mutex mu;
-    DevBuf seg_first, block_sum, seg2msg, ctrl;
+    DevBuf seg_first, block_sum, seg2msg, seginfo, bhist, ctrl;
     // host-pointer staging
     DevBuf arena, offsets, lengths, seeds, out;
     // BMQCRC_F_TIME_KERNEL: event pairs around k_fold not yet reported
@@ -164,21 +167,39 @@ uint64_t max_segs_for(uint64_t n, uint64_t arena_bytes, uint32_t seg)
     return n + arena_bytes / seg + 64;
 }
 
+// Contiguous ranges of whole kPlanBlock tiles, at most kPlanMaxBlocks blocks.
+static void split_ranges(uint64_t items, uint64_t* per, uint32_t* blocks)
+{
+    const uint64_t tiles = std::max<uint64_t>((items + kPlanBlock - 1) / kPlanBlock, 1);
+    const uint64_t nb = std::min<uint64_t>(tiles, kPlanMaxBlocks);
+    const uint64_t tiles_per = (tiles + nb - 1) / nb;
+    *per = tiles_per * kPlanBlock;
+    *blocks = (uint32_t)((tiles + tiles_per - 1) / tiles_per);
+}
+
 int plan_ws(Workspace* w, uint64_t n, uint64_t arena_bytes, uint32_t seg, BatchArgs* a)
 {
-    const uint64_t nblocks = (n + kPlanBlock - 1) / kPlanBlock;
     const uint64_t max_segs = max_segs_for(n, arena_bytes, seg);
+    split_ranges(n, &a->per_msg, &a->nblocks);
+    split_ranges(max_segs, &a->per_seg, &a->nblocks_seg);
     int rc;
     if ((rc = w->seg_first.ensure(4 * std::max<uint64_t>(n, 1))) ||
-        (rc = w->block_sum.ensure(8 * std::max<uint64_t>(nblocks, 1))) ||
-        (rc = w->seg2msg.ensure(4 * max_segs)) || (rc = w->ctrl.ensure(sizeof(PlanCtrl)))) {
+        (rc = w->block_sum.ensure(12ull * kPlanMaxBlocks)) ||
+        (rc = w->seg2msg.ensure(4 * max_segs)) || (rc = w->seginfo.ensure(8 * max_segs)) ||
+        (rc = w->bhist.ensure(4ull * kBuckets * kPlanMaxBlocks)) ||
+        (rc = w->ctrl.ensure(sizeof(PlanCtrl)))) {
         return rc;
+    }
+    if (w->ctrl.fresh) {
+        // last-block-done tickets must start at zero (the kernels reset them)
+        HIP_TRY(hipMemset(w->ctrl.p, 0, w->ctrl.bytes));
     }
     a->seg_first = (uint32_t*)w->seg_first.p;
     a->block_sum = (uint32_t*)w->block_sum.p;
     a->seg2msg = (uint32_t*)w->seg2msg.p;
+    a->seginfo = (uint32_t*)w->seginfo.p;
+    a->bhist = (uint32_t*)w->bhist.p;
     a->ctrl = (PlanCtrl*)w->ctrl.p;
-    a->nblocks = (uint32_t)nblocks;
     a->max_segs = max_segs;
     return 0;
 }

@@ -15,15 +15,21 @@ constexpr int kLdsBytes = kWavesPerBlock * kSlots * kSlotBytes;  // 64 KiB per b
 constexpr int kTabBytes = 8 * 256 * 4;  // remainder-reduction slicing tables (LDS)
 constexpr uint32_t kDefaultSegBytes = 16384;
 constexpr int kPlanBlock = 1024;
+constexpr int kPlanMaxBlocks = 256;  // planner grids stride over contiguous ranges
 
-// Control words written by the planner (device memory, 4 x u32).
-//   [0] total segments   [1] 1 if every message is exactly one segment
-//   [2] number of 64-segment groups
+constexpr int kBuckets = 16;            // segment size classes: floor(log2(lines))
+
+// Control words written by the planner (device memory).
 struct PlanCtrl {
-    uint32_t total_segs;
-    uint32_t identity;
-    uint32_t ngroups;
-    uint32_t pad;
+    uint32_t total_segs;   // number of segments in the batch
+    uint32_t identity;     // 1: every message is exactly one segment (segment g = message g)
+    uint32_t sorted;       // 1: seginfo lists the segments grouped by size class
+    uint32_t ngroups;      // ceil(total_segs / 64)
+    uint32_t ticket_plan;  // last-block-done tickets (zeroed at allocation, reset by the
+    uint32_t ticket_hist;  //   last block of each launch)
+    uint32_t overflow;     // total_segs > max_segs: segment -> message by binary search
+    uint32_t nseg_uniform; // > 0: every message has exactly this many segments
+                           //     (segment g = message g / u, part g % u; no emit/sort)
 };
 
 struct BatchArgs {
@@ -32,17 +38,21 @@ struct BatchArgs {
     const uint32_t* lengths;   // device, n
     const uint32_t* seeds;     // device, n, or nullptr (all zero)
     uint32_t* out;             // device, n
-    uint32_t* seg_first;       // workspace, n (exclusive prefix of segment counts)
-    uint32_t* block_sum;       // workspace, 2 * nblocks
-    uint32_t* seg2msg;         // workspace, max_segs
+    uint32_t* seg_first;       // workspace, n: block-local exclusive prefix of segment counts
+    uint32_t* block_sum;       // workspace, 3 * nblocks: [sums | non-1 counts | block offsets]
+    uint32_t* seg2msg;         // workspace, max_segs: segment -> message
+    uint32_t* seginfo;         // workspace, 2 * max_segs: (message, k) in size-class order
+    uint32_t* bhist;           // workspace, kBuckets * nblocks_seg: histogram, then offsets
     PlanCtrl* ctrl;            // workspace
     uint64_t n;
-    uint32_t seg_bytes;
-    uint32_t nblocks;          // planner blocks = ceil(n / kPlanBlock)
     uint64_t max_segs;
+    uint64_t per_msg;          // messages per k_plan block (multiple of kPlanBlock)
+    uint64_t per_seg;          // segments per k_plan_emit/k_plan_scatter block (idem)
+    uint32_t seg_bytes;
+    uint32_t nblocks;          // k_plan blocks (<= kPlanMaxBlocks)
+    uint32_t nblocks_seg;      // k_plan_emit / k_plan_scatter blocks (<= kPlanMaxBlocks)
     uint32_t tune;             // experiment knobs (BMQCRC_TUNE env): bit0 disables nt LDS-DMA
                                // loads, bit1 selects a 1-block/CU grid
-    uint32_t pad;
 };
 
 }  // namespace bmqcrc

@@ -274,14 +274,18 @@ __device__ __forceinline__ void mask_round(uint32_t (&m)[32], int sR, int eR, bo
     "global_load_lds_dwordx4 %9, off" CP "\n\t"                                             \
     "s_mov_b32 m0, %0\n\t"
 
+// Lanes whose segment has no line r (finished, or none) all read one dummy
+// line shared by the wave, so ragged waves add ~1 line per instruction of
+// traffic instead of re-reading every finished segment's last line.
 template <bool NT>
 __device__ __forceinline__ void dma_round(uint32_t lds_dst, const uint64_t (&dbase)[8],
-                                          const uint32_t (&dlim)[8], uint32_t r)
+                                          const uint32_t (&nlines)[8], uint64_t dummy,
+                                          uint32_t r)
 {
     uint64_t s[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        s[i] = dbase[i] + ((uint64_t)min(r, dlim[i]) << 7);
+        s[i] = (r < nlines[i]) ? dbase[i] + ((uint64_t)r << 7) : dummy;
     }
     uint32_t keep;
     if (NT) {
@@ -299,19 +303,47 @@ __device__ __forceinline__ void dma_round(uint32_t lds_dst, const uint64_t (&dba
         : "memory", "scc");
 }
 
-// Binary search: last message i with seg_first[i] <= g (rare overflow path).
-__device__ uint32_t find_msg(const uint32_t* seg_first, uint64_t n, uint32_t g)
+// Global exclusive prefix of segment counts: block-local part + block offset.
+__device__ __forceinline__ uint32_t seg_first_g(const BatchArgs& a, uint64_t i)
 {
-    uint64_t lo = 0, hi = n;  // invariant: seg_first[lo] <= g < seg_first[hi] (hi==n: inf)
+    return a.seg_first[i] + a.block_sum[2u * a.nblocks + (uint32_t)(i / a.per_msg)];
+}
+
+// Binary search: last message i with seg_first(i) <= g.
+__device__ uint32_t find_msg(const BatchArgs& a, uint32_t g)
+{
+    uint64_t lo = 0, hi = a.n;  // invariant: first(lo) <= g < first(hi) (hi == n: inf)
     while (hi - lo > 1) {
         const uint64_t mid = (lo + hi) >> 1;
-        if (seg_first[mid] <= g) {
+        if (seg_first_g(a, mid) <= g) {
             lo = mid;
         } else {
             hi = mid;
         }
     }
     return (uint32_t)lo;
+}
+
+// Geometry of segment k of a message [mstart, mstart+len): byte range
+// [S, E) (internal boundaries 128-byte aligned), first line L0, lines of the
+// folded stream (covering the seed word of the first segment) and of data.
+struct SegGeom {
+    uint64_t S, E, L0;
+    uint32_t nl, nl_data;
+};
+
+__device__ __forceinline__ SegGeom seg_geom(uint64_t mstart, uint32_t len, uint32_t k,
+                                            uint32_t nseg, uint32_t SEG)
+{
+    SegGeom g;
+    const uint64_t mend = mstart + len;
+    g.S = (k == 0) ? mstart : ((mstart + (uint64_t)k * SEG) & ~127ull);
+    g.E = (k + 1 == nseg) ? mend : ((mstart + (uint64_t)(k + 1) * SEG) & ~127ull);
+    g.L0 = g.S & ~127ull;
+    const uint64_t need_end = (k == 0 && g.E < g.S + 4) ? g.S + 4 : g.E;
+    g.nl = (uint32_t)((need_end - g.L0 + 127u) >> 7);
+    g.nl_data = (uint32_t)((g.E - g.L0 + 127u) >> 7);
+    return g;
 }
 
 template <bool NT>
@@ -333,6 +365,8 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
 
     const uint32_t total = a.ctrl->total_segs;
     const uint32_t identity = a.ctrl->identity;
+    const uint32_t sorted = a.ctrl->sorted;
+    const uint32_t uni = a.ctrl->nseg_uniform;
     const uint32_t ngroups = (total + 63u) / 64u;
     const uint32_t SEG = a.seg_bytes;
     const uint64_t arena = (uint64_t)(uintptr_t)a.arena;
@@ -347,37 +381,44 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         uint32_t msg = 0, len = 0, seed = 0, k = 0;
         uint64_t off = 0;
         if (valid) {
-            msg = identity ? seg
-                           : (seg < a.max_segs ? a.seg2msg[seg] : find_msg(a.seg_first, a.n, seg));
+            if (identity) {
+                msg = seg;
+            } else if (uni) {
+                msg = seg / uni;
+                k = seg - msg * uni;
+            } else if (sorted) {
+                msg = a.seginfo[2u * seg];
+                k = a.seginfo[2u * seg + 1u];
+            } else {
+                msg = seg < a.max_segs ? a.seg2msg[seg] : find_msg(a, seg);
+                k = seg - seg_first_g(a, msg);
+            }
             off = a.offsets[msg];
             len = a.lengths[msg];
             seed = a.seeds ? a.seeds[msg] : 0u;
-            k = seg - a.seg_first[msg];
         }
         const uint32_t nseg = valid ? (len - 1u) / SEG + 1u : 0u;
         const uint64_t mstart = arena + off;
         const uint64_t mend = mstart + len;
-        const uint64_t S = (k == 0) ? mstart : ((mstart + (uint64_t)k * SEG) & ~127ull);
-        const uint64_t E = (k + 1 == nseg) ? mend : ((mstart + (uint64_t)(k + 1) * SEG) & ~127ull);
+        const SegGeom geo = seg_geom(mstart, len, k, nseg, SEG);
+        const uint64_t S = geo.S, E = geo.E, L0 = geo.L0;
         const bool first = valid && k == 0;
-        const uint64_t L0 = S & ~127ull;
-        const uint64_t need_end = (first && E < S + 4) ? S + 4 : E;
-        const uint32_t nl = valid ? (uint32_t)((need_end - L0 + 127u) >> 7) : 0u;
-        const uint32_t nl_data = valid ? (uint32_t)((E - L0 + 127u) >> 7) : 0u;
+        const uint32_t nl = valid ? geo.nl : 0u;
+        const uint32_t nl_data = valid ? geo.nl_data : 0u;
         const uint32_t R = wave_max(nl);
 
         // ------------------------------------------ DMA source per instruction
-        const uint64_t dummy = rfl64(L0);  // lane 0 always holds a valid segment here
+        // lane 0 always holds a valid segment here; its first line is the dummy
+        const uint64_t dummy = rfl64(L0) + 16u * ((uint32_t)lane & 7u);
         uint64_t dbase[8];
-        uint32_t dlim[8];
+        uint32_t dlim[8];  // lines of data of segment 8i + lane/8 (0: none)
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int src = 8 * i + (lane >> 3);
             const uint64_t l0 = shfl64(L0, src);
-            const uint32_t nd = (uint32_t)__shfl((int)nl_data, src);
             const uint32_t p = ((uint32_t)lane & 7u) ^ ((4u * i + ((uint32_t)lane >> 4)) & 7u);
-            dbase[i] = nd ? l0 + 16u * p : dummy;
-            dlim[i] = nd ? nd - 1u : 0u;
+            dbase[i] = l0 + 16u * p;
+            dlim[i] = (uint32_t)__shfl((int)nl_data, src);
         }
 
         // ------------------------------------------------------ fold rounds
@@ -390,9 +431,9 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         const uint32_t c0 = ~seed;
         const uint64_t inj_end = first ? S + 4 : S;
 
-        dma_round<NT>(wave_lds, dbase, dlim, 0);
+        dma_round<NT>(wave_lds, dbase, dlim, dummy, 0);
         if (R > 1) {
-            dma_round<NT>(wave_lds + kSlotBytes, dbase, dlim, 1);
+            dma_round<NT>(wave_lds + kSlotBytes, dbase, dlim, dummy, 1);
         }
         for (uint32_t r = 0; r < R; ++r) {
             const uint32_t slot = wave_lds + (r & 1u) * kSlotBytes;
@@ -411,7 +452,7 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
                 m[4 * kk + 3] = v.w;
             }
             if (r + 2 < R) {
-                dma_round<NT>(slot, dbase, dlim, r + 2);
+                dma_round<NT>(slot, dbase, dlim, dummy, r + 2);
             }
             const uint64_t p0 = L0 + ((uint64_t)r << 7);
             if (r < nl && (p0 < inj_end || p0 + 128u > E)) {
@@ -470,20 +511,40 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
 }
 
 // ---------------------------------------------------------------- planner
-__global__ __launch_bounds__(kPlanBlock) void k_plan_count(BatchArgs a)
+// Last-block-done hand-off without fences (MI355X_MICROARCH.md "Workgroup
+// dispatch ... visibility", valid forms, write-through row): thread 0 of every
+// block publishes its words with agent-scope relaxed (sc1, write-through)
+// stores, waits vmcnt(0), then takes a relaxed agent ticket; the block that
+// draws the last ticket reads the published words with sc1 loads only.
+__device__ __forceinline__ void publish(uint32_t* p, uint32_t v)
 {
-    __shared__ uint32_t wsum[kPlanBlock / 64];
-    __shared__ uint32_t wnon1[kPlanBlock / 64];
-    const uint64_t i = (uint64_t)blockIdx.x * kPlanBlock + threadIdx.x;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t ns = 0;
-    if (i < a.n) {
-        const uint32_t len = a.lengths[i];
-        ns = len ? (len - 1u) / a.seg_bytes + 1u : 0u;
-        a.out[i] = len ? 0u : (a.seeds ? a.seeds[i] : 0u);
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint32_t consume(const uint32_t* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Called by all threads after thread 0 has published.  True in the last block.
+__device__ __forceinline__ bool last_block_arrival(uint32_t* ticket, uint32_t nblocks,
+                                                   uint32_t* flag_lds)
+{
+    if (threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t t =
+            __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *flag_lds = (t == nblocks - 1) ? 1u : 0u;
     }
-    const uint64_t non1_mask = __ballot(i < a.n && ns != 1u);
-    uint32_t x = ns;
+    __syncthreads();
+    return *flag_lds != 0;
+}
+
+// Block-wide exclusive scan of v (1024 threads); returns the block total.
+__device__ __forceinline__ uint32_t block_scan_1024(uint32_t v, uint32_t* excl, uint32_t* wsum)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t x = v;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t y = (uint32_t)__shfl_up((int)x, o);
@@ -493,100 +554,257 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_count(BatchArgs a)
     }
     if (lane == 63) {
         wsum[wave] = x;
-        wnon1[wave] = (uint32_t)__popcll(non1_mask);
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t run = 0, non1 = 0;
-        for (int w = 0; w < kPlanBlock / 64; ++w) {
-            const uint32_t t = wsum[w];
-            wsum[w] = run;
-            run += t;
-            non1 += wnon1[w];
+    if (threadIdx.x < 16) {
+        uint32_t w = wsum[threadIdx.x], y = w;
+        for (int o = 1; o < 16; o <<= 1) {
+            const uint32_t z = (uint32_t)__shfl_up((int)y, o, 16);
+            if ((int)threadIdx.x >= o) {
+                y += z;
+            }
         }
-        a.block_sum[blockIdx.x] = run;
-        a.block_sum[a.nblocks + blockIdx.x] = non1;
+        wsum[16 + threadIdx.x] = y - w;  // exclusive wave prefix
+        if (threadIdx.x == 15) {
+            wsum[32] = y;
+        }
     }
     __syncthreads();
-    if (i < a.n) {
-        a.seg_first[i] = x - ns + wsum[wave];
-    }
+    *excl = x - v + wsum[16 + wave];
+    const uint32_t tot = wsum[32];
+    __syncthreads();
+    return tot;
 }
 
-__global__ __launch_bounds__(1024) void k_plan_scan(BatchArgs a)
+// K1: segment counts per message, block-local prefix over the block's
+// contiguous message range, and (last block) the prefix over blocks + totals.
+__global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
 {
-    __shared__ uint32_t wsum[16];
-    __shared__ uint32_t carry_s, non1_s;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __shared__ uint32_t wsum[40];
+    __shared__ uint32_t sh[4];
     if (threadIdx.x == 0) {
-        carry_s = 0;
-        non1_s = 0;
+        sh[1] = 0;            // messages with != 1 segment
+        sh[2] = 0xffffffffu;  // min segments per message
+        sh[3] = 0;            // max segments per message
     }
     __syncthreads();
-    for (uint32_t base = 0; base < a.nblocks; base += 1024) {
-        const uint32_t j = base + threadIdx.x;
-        const uint32_t v = j < a.nblocks ? a.block_sum[j] : 0u;
-        const uint32_t nn = j < a.nblocks ? a.block_sum[a.nblocks + j] : 0u;
-        if (nn) {
-            atomicAdd(&non1_s, nn);
+    const uint64_t lo = (uint64_t)blockIdx.x * a.per_msg;
+    const uint64_t hi = min(lo + a.per_msg, a.n);
+    uint32_t carry = 0;
+    for (uint64_t base = lo; base < hi; base += kPlanBlock) {
+        const uint64_t i = base + threadIdx.x;
+        uint32_t ns = 0;
+        if (i < hi) {
+            const uint32_t len = a.lengths[i];
+            ns = len ? (len - 1u) / a.seg_bytes + 1u : 0u;
+            a.out[i] = len ? 0u : (a.seeds ? a.seeds[i] : 0u);
         }
-        uint32_t x = v;
+        // block-level min / max / count(!=1) via wave reductions
+        uint32_t mn = i < hi ? ns : 0xffffffffu, mx = ns;
+        const uint64_t non1 = __ballot(i < hi && ns != 1u);
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)x, o);
-            if (lane >= o) {
-                x += y;
+        for (int o = 32; o > 0; o >>= 1) {
+            mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
+            mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+        }
+        if ((threadIdx.x & 63) == 0) {
+            atomicMin(&sh[2], mn);
+            atomicMax(&sh[3], mx);
+            if (non1) {
+                atomicAdd(&sh[1], (uint32_t)__popcll(non1));
             }
         }
-        if (lane == 63) {
-            wsum[wave] = x;
+        uint32_t excl;
+        const uint32_t tot = block_scan_1024(ns, &excl, wsum);
+        if (i < hi) {
+            a.seg_first[i] = carry + excl;
         }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t run = 0;
-            for (int w = 0; w < 16; ++w) {
-                const uint32_t t = wsum[w];
-                wsum[w] = run;
-                run += t;
-            }
-        }
-        __syncthreads();
-        const uint32_t carry = carry_s;
-        if (j < a.nblocks) {
-            a.block_sum[j] = carry + wsum[wave] + x - v;
-        }
-        __syncthreads();
-        if (threadIdx.x == 1023) {
-            carry_s = carry + wsum[wave] + x;
-        }
-        __syncthreads();
+        carry += tot;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        publish(&a.block_sum[blockIdx.x], carry);
+        publish(&a.block_sum[a.nblocks + blockIdx.x], sh[1]);
+        publish(&a.block_sum[2u * a.nblocks + blockIdx.x], sh[2] == sh[3] ? sh[2] : 0xffffffffu);
+    }
+    if (!last_block_arrival(&a.ctrl->ticket_plan, a.nblocks, &sh[0])) {
+        return;
+    }
+    // last block (nblocks <= 1024): scan of the block totals, sc1 loads
+    const uint32_t j = threadIdx.x;
+    const uint32_t v = j < a.nblocks ? consume(&a.block_sum[j]) : 0u;
+    const uint32_t nn = j < a.nblocks ? consume(&a.block_sum[a.nblocks + j]) : 0u;
+    const uint32_t u0 = consume(&a.block_sum[2u * a.nblocks]);
+    const uint32_t u = j < a.nblocks ? consume(&a.block_sum[2u * a.nblocks + j]) : u0;
+    const int mismatch = __syncthreads_or(u != u0);
+    uint32_t ex;
+    const uint32_t total = block_scan_1024(v, &ex, wsum);
+    uint32_t ex2;
+    const uint32_t non1 = block_scan_1024(nn, &ex2, wsum);
+    if (j < a.nblocks) {
+        a.block_sum[2u * a.nblocks + j] = ex;  // block offsets (read by later launches)
     }
     if (threadIdx.x == 0) {
-        a.ctrl->total_segs = carry_s;
-        a.ctrl->identity = (non1_s == 0) ? 1u : 0u;
-        a.ctrl->ngroups = (carry_s + 63u) / 64u;
-        a.ctrl->pad = 0;
+        a.ctrl->total_segs = total;
+        a.ctrl->identity = (non1 == 0) ? 1u : 0u;
+        a.ctrl->ngroups = (total + 63u) / 64u;
+        a.ctrl->overflow = (total > a.max_segs) ? 1u : 0u;
+        a.ctrl->nseg_uniform = (!mismatch && u0 != 0xffffffffu && u0 != 0u) ? u0 : 0u;
+        a.ctrl->sorted = 0;
+        a.ctrl->ticket_plan = 0;  // for the next launch
     }
 }
 
-__global__ void k_plan_fix(BatchArgs a)
+__device__ __forceinline__ uint32_t size_class(uint32_t nl)
 {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < a.n) {
-        a.seg_first[i] += a.block_sum[i / kPlanBlock];
-    }
+    const uint32_t b = 31u - __clz(nl | 1u);
+    return b < kBuckets - 1 ? b : kBuckets - 1;
 }
 
-__global__ void k_plan_emit(BatchArgs a)
+// K2: segment -> message (binary search over the prefix), per-block size-class
+// histogram over the block's contiguous segment range, and (last block)
+// bucket-major offsets for the sort.
+__device__ __forceinline__ uint32_t seg_class(const BatchArgs& a, uint32_t msg, uint32_t k)
 {
-    if (a.ctrl->identity) {
-        return;
+    const uint32_t len = a.lengths[msg];
+    const uint32_t nseg = (len - 1u) / a.seg_bytes + 1u;
+    const SegGeom geo =
+        seg_geom((uint64_t)(uintptr_t)a.arena + a.offsets[msg], len, k, nseg, a.seg_bytes);
+    return size_class(geo.nl);
+}
+
+__global__ __launch_bounds__(kPlanBlock) void k_plan_emit(BatchArgs a)
+{
+    __shared__ uint32_t hist[kBuckets];
+    __shared__ uint32_t flag;
+    if (a.ctrl->identity || a.ctrl->nseg_uniform) {
+        return;  // closed-form mapping; uniform across the grid: nobody takes a ticket
     }
     const uint64_t total = a.ctrl->total_segs;
     const uint64_t lim = total < a.max_segs ? total : a.max_segs;
-    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < lim;
-         g += (uint64_t)gridDim.x * blockDim.x) {
-        a.seg2msg[g] = find_msg(a.seg_first, a.n, (uint32_t)g);
+    if (threadIdx.x < kBuckets) {
+        hist[threadIdx.x] = 0;
+    }
+    __syncthreads();
+    const uint64_t lo = (uint64_t)blockIdx.x * a.per_seg;
+    const uint64_t hi = min(lo + a.per_seg, lim);
+    for (uint64_t g = lo + threadIdx.x; g < hi; g += kPlanBlock) {
+        const uint32_t msg = find_msg(a, (uint32_t)g);
+        const uint32_t k = (uint32_t)g - seg_first_g(a, msg);
+        a.seg2msg[g] = msg;
+        atomicAdd(&hist[seg_class(a, msg, k)], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int c = 0; c < kBuckets; ++c) {
+            publish(&a.bhist[(uint64_t)blockIdx.x * kBuckets + c], hist[c]);
+        }
+    }
+    if (!last_block_arrival(&a.ctrl->ticket_hist, a.nblocks_seg, &flag)) {
+        return;
+    }
+    // last block: bucket-major exclusive offsets over (bucket, block).  Wave c
+    // scans bucket c over the blocks; thread 0 then scans the bucket totals.
+    __shared__ uint32_t btot[kBuckets];
+    __shared__ uint32_t bbase[kBuckets];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (wave < kBuckets) {
+        uint32_t run = 0;
+        for (uint32_t base = 0; base < a.nblocks_seg; base += 64) {
+            const uint32_t b = base + lane;
+            const uint32_t v =
+                b < a.nblocks_seg ? consume(&a.bhist[(uint64_t)b * kBuckets + wave]) : 0u;
+            uint32_t x = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+                if (lane >= o) {
+                    x += y;
+                }
+            }
+            if (b < a.nblocks_seg) {
+                a.bhist[(uint64_t)b * kBuckets + wave] = run + x - v;
+            }
+            run += (uint32_t)__shfl((int)x, 63);
+        }
+        if (lane == 0) {
+            btot[wave] = run;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0, used = 0;
+        for (int c = 0; c < kBuckets; ++c) {
+            bbase[c] = acc;
+            acc += btot[c];
+            used += btot[c] ? 1u : 0u;
+        }
+        a.ctrl->sorted = (used > 1 && !a.ctrl->overflow) ? 1u : 0u;
+        a.ctrl->ticket_hist = 0;
+    }
+    __syncthreads();
+    if (wave < kBuckets) {
+        for (uint32_t b = lane; b < a.nblocks_seg; b += 64) {
+            a.bhist[(uint64_t)b * kBuckets + wave] += bbase[wave];
+        }
+    }
+}
+
+// K3: stable scatter of (message, k) into size-class order; each block walks
+// the same segment range in the same order as in K2.
+__global__ __launch_bounds__(kPlanBlock) void k_plan_scatter(BatchArgs a)
+{
+    __shared__ uint32_t wcnt[16][kBuckets];
+    __shared__ uint32_t run[kBuckets];
+    if (a.ctrl->identity || a.ctrl->nseg_uniform || !a.ctrl->sorted) {
+        return;
+    }
+    const uint64_t total = a.ctrl->total_segs;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (threadIdx.x < kBuckets) {
+        run[threadIdx.x] = a.bhist[(uint64_t)blockIdx.x * kBuckets + threadIdx.x];
+    }
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const uint64_t lo = (uint64_t)blockIdx.x * a.per_seg;
+    const uint64_t hi = min(lo + a.per_seg, total);
+    for (uint64_t base = lo; base < hi; base += kPlanBlock) {
+        const uint64_t g = base + threadIdx.x;
+        uint32_t msg = 0, k = 0, cls = kBuckets;  // kBuckets: no segment
+        if (g < hi) {
+            msg = a.seg2msg[g];
+            k = (uint32_t)g - seg_first_g(a, msg);
+            cls = seg_class(a, msg, k);
+        }
+        uint32_t rank = 0;
+#pragma unroll
+        for (int c = 0; c < kBuckets; ++c) {
+            const uint64_t m = __ballot(cls == (uint32_t)c);
+            if (cls == (uint32_t)c) {
+                rank = (uint32_t)__popcll(m & lt);
+            }
+            if (lane == 0) {
+                wcnt[wave][c] = (uint32_t)__popcll(m);
+            }
+        }
+        __syncthreads();
+        if (cls < kBuckets) {
+            uint32_t before = run[cls];
+            for (int w = 0; w < wave; ++w) {
+                before += wcnt[w][cls];
+            }
+            const uint64_t pos = (uint64_t)before + rank;
+            a.seginfo[2u * pos] = msg;
+            a.seginfo[2u * pos + 1u] = k;
+        }
+        __syncthreads();
+        if (threadIdx.x < kBuckets) {
+            uint32_t t = 0;
+            for (int w = 0; w < 16; ++w) {
+                t += wcnt[w][threadIdx.x];
+            }
+            run[threadIdx.x] += t;
+        }
+        __syncthreads();
     }
 }
 
@@ -628,14 +846,9 @@ extern "C" int bmqcrc_launch_batch(const BatchArgs* a, void* stream, int num_cus
     if (a->n == 0) {
         return 0;
     }
-    hipLaunchKernelGGL(k_plan_count, dim3(a->nblocks), dim3(kPlanBlock), 0, s, *a);
-    hipLaunchKernelGGL(k_plan_scan, dim3(1), dim3(1024), 0, s, *a);
-    hipLaunchKernelGGL(k_plan_fix, dim3(a->nblocks), dim3(kPlanBlock), 0, s, *a);
-    uint64_t emit_blocks = (a->max_segs + 255) / 256;
-    if (emit_blocks > 4096) {
-        emit_blocks = 4096;
-    }
-    hipLaunchKernelGGL(k_plan_emit, dim3((unsigned)emit_blocks), dim3(256), 0, s, *a);
+    hipLaunchKernelGGL(k_plan, dim3(a->nblocks), dim3(kPlanBlock), 0, s, *a);
+    hipLaunchKernelGGL(k_plan_emit, dim3(a->nblocks_seg), dim3(kPlanBlock), 0, s, *a);
+    hipLaunchKernelGGL(k_plan_scatter, dim3(a->nblocks_seg), dim3(kPlanBlock), 0, s, *a);
     const uint64_t max_groups = (a->max_segs + 63) / 64;
     uint64_t grid = (max_groups + kWavesPerBlock - 1) / kWavesPerBlock;
     const uint64_t cap = (uint64_t)(num_cus > 0 ? num_cus : 256) * (a->tune & 2u ? 1u : 2u);
