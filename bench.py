@@ -153,6 +153,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo")
+    # BENCH_DEVICE pins every rank to one GPU: only for rehearsing the
+    # multi-process path on a one-GPU box (never used for reported numbers).
+    local = int(os.environ.get("BENCH_DEVICE", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
