@@ -56,6 +56,12 @@ lib.bmqcrc_combine.restype = _u32
 lib.bmqcrc_combine.argtypes = [_u32, _u32, _u64]
 lib.bmqcrc_crc32c_batch.restype = _int
 lib.bmqcrc_crc32c_batch.argtypes = [_vp, _u64, _vp, _vp, _vp, _vp, _u64, ctypes.POINTER(Opts)]
+lib.bmqcrc_crc32c_verify.restype = _int
+lib.bmqcrc_crc32c_verify.argtypes = [_vp, _u64, _vp, _vp, _vp, _u64, ctypes.POINTER(_u64), _vp,
+                                     _u64, ctypes.POINTER(Opts)]
+lib.bmqcrc_crc32c_blobs.restype = _int
+lib.bmqcrc_crc32c_blobs.argtypes = [_vp, _u64, _vp, _vp, _u64, _vp, _vp, _vp, _u64,
+                                    ctypes.POINTER(Opts)]
 lib.bmqcrc_crc32c_batch_multi.restype = _int
 lib.bmqcrc_crc32c_batch_multi.argtypes = [_vp, _u64, _vp, _vp, _vp, _vp, _u64, _vp, _int, _u32]
 lib.bmqcrc_reserve.restype = _int

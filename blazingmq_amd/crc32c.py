@@ -100,6 +100,16 @@ class Crc32c:
         return _native.lib.bmqcrc_combine(crc_a & 0xFFFFFFFF, crc_b & 0xFFFFFFFF, len_b)
 
     @staticmethod
+    def verify_batch(arena, offsets, lengths, expected, bad_cap=1 << 20, seg_bytes=0):
+        """Batched recovery check (bmqcrc_crc32c_verify): (n_bad, bad indices)."""
+        return verify_batch(arena, offsets, lengths, expected, bad_cap, seg_bytes)
+
+    @staticmethod
+    def calculate_blobs(blobs, seeds=None, seg_bytes=0):
+        """Batched Blob overload (bmqcrc_crc32c_blobs) on the GPU."""
+        return calculate_blobs(blobs, seeds, seg_bytes)
+
+    @staticmethod
     def calculate_batch(arena, offsets, lengths, seeds=None, out=None, *, seg_bytes=0,
                         device=None, stream=None, sync=True, time_kernel=False):
         """Batched CRC32-C of messages ``arena[offsets[i] : offsets[i]+lengths[i]]``.
@@ -164,6 +174,62 @@ def _batch_host(arena, offsets, lengths, seeds, out, seg_bytes, device):
         a.ctypes.data if a.size else None, a.size, off.ctypes.data, ln.ctypes.data,
         sd.ctypes.data if sd is not None else None, res.ctypes.data, off.size, ctypes.byref(o)))
     return res
+
+
+def _u8_host(arena):
+    if isinstance(arena, (bytes, bytearray, memoryview)):
+        return np.frombuffer(bytes(arena), dtype=np.uint8)
+    return np.ascontiguousarray(arena).view(np.uint8).reshape(-1)
+
+
+def verify_batch(arena, offsets, lengths, expected, bad_cap=1 << 20, seg_bytes=0, device=None):
+    """GPU batch CRC of every message compared on the device with `expected`.
+
+    Returns (n_bad, bad_index ndarray[uint64], ascending, at most bad_cap)."""
+    a = _u8_host(arena)
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    ln = np.ascontiguousarray(lengths, dtype=np.uint32)
+    ex = np.ascontiguousarray(expected, dtype=np.uint32)
+    if not (off.shape == ln.shape == ex.shape):
+        raise ValueError("offsets/lengths/expected size mismatch")
+    nbad = ctypes.c_uint64()
+    idx = np.zeros(max(int(bad_cap), 1), dtype=np.uint64)
+    o = _native.make_opts(device=-1 if device is None else device, seg_bytes=seg_bytes)
+    _native.check(_native.lib.bmqcrc_crc32c_verify(
+        a.ctypes.data if a.size else None, a.size, off.ctypes.data, ln.ctypes.data,
+        ex.ctypes.data, off.size, ctypes.byref(nbad), idx.ctypes.data, int(bad_cap),
+        ctypes.byref(o)))
+    return int(nbad.value), idx[:min(int(nbad.value), int(bad_cap))].copy()
+
+
+def calculate_blobs(blobs, seeds=None, seg_bytes=0, device=None):
+    """``bmqp::Crc32c::calculate(blob, seed)`` for a list of Blob on the GPU:
+    buffers are gathered into one staging arena, CRC'd per buffer and chained
+    on the device.  Returns ndarray[uint32]."""
+    bufs, lens, first = [], [], [0]
+    for b in blobs:
+        nb = b.num_data_buffers()
+        for i in range(nb):
+            data = b.buffer(i)
+            n = len(data) if i < nb - 1 else b.last_data_buffer_length()
+            bufs.append(bytes(data[:n]))
+            lens.append(n)
+        first.append(len(lens))
+    arena = np.frombuffer(b"".join(bufs) + b"\0", dtype=np.uint8)
+    offs = np.zeros(len(lens), dtype=np.uint64)
+    if len(lens) > 1:
+        offs[1:] = np.cumsum(np.asarray(lens[:-1], dtype=np.uint64))
+    ln = np.asarray(lens, dtype=np.uint32)
+    fb = np.asarray(first, dtype=np.uint64)
+    sd = None if seeds is None else np.ascontiguousarray(seeds, dtype=np.uint32)
+    out = np.empty(len(blobs), dtype=np.uint32)
+    o = _native.make_opts(device=-1 if device is None else device, seg_bytes=seg_bytes)
+    _native.check(_native.lib.bmqcrc_crc32c_blobs(
+        arena.ctypes.data, arena.size, offs.ctypes.data if ln.size else None,
+        ln.ctypes.data if ln.size else None, ln.size, fb.ctypes.data,
+        sd.ctypes.data if sd is not None else None, out.ctypes.data, len(blobs),
+        ctypes.byref(o)))
+    return out
 
 
 def calculate_batch_multi(arena, offsets, lengths, seeds=None, devices=None, seg_bytes=0):

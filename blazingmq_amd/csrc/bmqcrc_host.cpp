@@ -83,6 +83,8 @@ struct Workspace {
     DevBuf seg_first, block_sum, seg2msg, seginfo, bhist, ctrl;
     // host-pointer staging
     DevBuf arena, offsets, lengths, seeds, out;
+    // verify / blobs
+    DevBuf expected, vcount, vidx, buf_crc, first_buf;
     // BMQCRC_F_TIME_KERNEL: event pairs around k_fold not yet reported
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timing, spare;
     ~Workspace()
@@ -215,20 +217,32 @@ int check_seg(uint32_t* seg)
     return 0;
 }
 
-int batch_one(int dev, void* user_stream, uint32_t flags, uint32_t seg, const void* arena,
-              uint64_t arena_bytes, const uint64_t* offsets, const uint32_t* lengths,
-              const uint32_t* seeds, uint32_t* out, uint64_t n)
-{
+struct Ctx {
+    int dev = 0;
     DeviceState* st = nullptr;
-    int rc = device_state(dev, &st);
+    hipStream_t s = nullptr;
+    Workspace* w = nullptr;
+};
+
+int open_ctx(int dev, void* user_stream, Ctx* c)
+{
+    int rc = device_state(dev, &c->st);
     if (rc) {
         return rc;
     }
     HIP_TRY(hipSetDevice(dev));
-    hipStream_t s = user_stream ? (hipStream_t)user_stream : st->own_stream;
-    Workspace* w = workspace(dev, user_stream);
-    std::lock_guard<std::mutex> g(w->mu);
+    c->dev = dev;
+    c->s = user_stream ? (hipStream_t)user_stream : c->st->own_stream;
+    c->w = workspace(dev, user_stream);
+    return 0;
+}
 
+// Enqueue planner + fold on device pointers (caller holds c.w->mu).
+int run_batch(Ctx& c, uint32_t flags, uint32_t seg, const void* arena, uint64_t arena_bytes,
+              const uint64_t* offsets, const uint32_t* lengths, const uint32_t* seeds,
+              uint32_t* out, uint64_t n)
+{
+    Workspace* w = c.w;
     BatchArgs a;
     memset(&a, 0, sizeof(a));
     a.n = n;
@@ -238,34 +252,15 @@ int batch_one(int dev, void* user_stream, uint32_t flags, uint32_t seg, const vo
         return e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
     }();
     a.tune = tune;
+    int rc;
     if ((rc = plan_ws(w, n, arena_bytes, seg, &a))) {
         return rc;
     }
-    const bool dev_ptrs = (flags & BMQCRC_F_DEVICE_PTRS) != 0;
-    if (dev_ptrs) {
-        a.arena = (const uint8_t*)arena;
-        a.offsets = offsets;
-        a.lengths = lengths;
-        a.seeds = seeds;
-        a.out = out;
-    } else {
-        if ((rc = w->arena.ensure(arena_bytes + 16)) || (rc = w->offsets.ensure(8 * n)) ||
-            (rc = w->lengths.ensure(4 * n)) || (rc = w->out.ensure(4 * n)) ||
-            (seeds && (rc = w->seeds.ensure(4 * n)))) {
-            return rc;
-        }
-        HIP_TRY(hipMemcpyAsync(w->arena.p, arena, arena_bytes, hipMemcpyHostToDevice, s));
-        HIP_TRY(hipMemcpyAsync(w->offsets.p, offsets, 8 * n, hipMemcpyHostToDevice, s));
-        HIP_TRY(hipMemcpyAsync(w->lengths.p, lengths, 4 * n, hipMemcpyHostToDevice, s));
-        if (seeds) {
-            HIP_TRY(hipMemcpyAsync(w->seeds.p, seeds, 4 * n, hipMemcpyHostToDevice, s));
-        }
-        a.arena = (const uint8_t*)w->arena.p;
-        a.offsets = (const uint64_t*)w->offsets.p;
-        a.lengths = (const uint32_t*)w->lengths.p;
-        a.seeds = seeds ? (const uint32_t*)w->seeds.p : nullptr;
-        a.out = (uint32_t*)w->out.p;
-    }
+    a.arena = (const uint8_t*)arena;
+    a.offsets = offsets;
+    a.lengths = lengths;
+    a.seeds = seeds;
+    a.out = out;
     void* ev0 = nullptr;
     void* ev1 = nullptr;
     if (flags & BMQCRC_F_TIME_KERNEL) {
@@ -281,15 +276,86 @@ int batch_one(int dev, void* user_stream, uint32_t flags, uint32_t seg, const vo
         ev0 = (void*)ev.first;
         ev1 = (void*)ev.second;
     }
-    if (bmqcrc_launch_batch(&a, (void*)s, st->num_cus, ev0, ev1) != 0) {
+    if (bmqcrc_launch_batch(&a, (void*)c.s, c.st->num_cus, ev0, ev1) != 0) {
         return fail(BMQCRC_EIO, std::string("kernel launch failed: ") +
                                     hipGetErrorString(hipGetLastError()));
     }
-    if (!dev_ptrs) {
-        HIP_TRY(hipMemcpyAsync(out, w->out.p, 4 * n, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-    } else if (!(flags & BMQCRC_F_ASYNC)) {
-        HIP_TRY(hipStreamSynchronize(s));
+    return 0;
+}
+
+// Stage host arrays into workspace buffers (async on c.s).
+int stage(Ctx& c, DevBuf& buf, const void* host, uint64_t bytes)
+{
+    int rc = buf.ensure(bytes + 16);
+    if (rc) {
+        return rc;
+    }
+    if (bytes) {
+        HIP_TRY(hipMemcpyAsync(buf.p, host, bytes, hipMemcpyHostToDevice, c.s));
+    }
+    return 0;
+}
+
+int batch_one(int dev, void* user_stream, uint32_t flags, uint32_t seg, const void* arena,
+              uint64_t arena_bytes, const uint64_t* offsets, const uint32_t* lengths,
+              const uint32_t* seeds, uint32_t* out, uint64_t n)
+{
+    Ctx c;
+    int rc = open_ctx(dev, user_stream, &c);
+    if (rc) {
+        return rc;
+    }
+    Workspace* w = c.w;
+    std::lock_guard<std::mutex> g(w->mu);
+    const bool dev_ptrs = (flags & BMQCRC_F_DEVICE_PTRS) != 0;
+    if (dev_ptrs) {
+        if ((rc = run_batch(c, flags, seg, arena, arena_bytes, offsets, lengths, seeds, out, n))) {
+            return rc;
+        }
+        if (!(flags & BMQCRC_F_ASYNC)) {
+            HIP_TRY(hipStreamSynchronize(c.s));
+        }
+        return 0;
+    }
+    if ((rc = stage(c, w->arena, arena, arena_bytes)) ||
+        (rc = stage(c, w->offsets, offsets, 8 * n)) || (rc = stage(c, w->lengths, lengths, 4 * n)) ||
+        (seeds && (rc = stage(c, w->seeds, seeds, 4 * n))) || (rc = w->out.ensure(4 * n))) {
+        return rc;
+    }
+    if ((rc = run_batch(c, flags, seg, w->arena.p, arena_bytes, (const uint64_t*)w->offsets.p,
+                        (const uint32_t*)w->lengths.p,
+                        seeds ? (const uint32_t*)w->seeds.p : nullptr, (uint32_t*)w->out.p, n))) {
+        return rc;
+    }
+    HIP_TRY(hipMemcpyAsync(out, w->out.p, 4 * n, hipMemcpyDeviceToHost, c.s));
+    HIP_TRY(hipStreamSynchronize(c.s));
+    return 0;
+}
+
+int parse_opts(const bmqcrc_opts* opts, bmqcrc_opts* o, uint32_t* seg, int* dev)
+{
+    memset(o, 0, sizeof(*o));
+    o->device = -1;
+    if (opts) {
+        memcpy(o, opts,
+               std::min<size_t>(sizeof(*o), opts->struct_size ? opts->struct_size : sizeof(*o)));
+    }
+    *seg = o->seg_bytes;
+    int rc;
+    if ((rc = check_seg(seg)) || (rc = resolve_device(o->device, dev))) {
+        return rc;
+    }
+    return 0;
+}
+
+int check_ranges(const uint64_t* offsets, const uint32_t* lengths, uint64_t n,
+                 uint64_t arena_bytes)
+{
+    for (uint64_t i = 0; i < n; ++i) {
+        if (offsets[i] > arena_bytes || lengths[i] > arena_bytes - offsets[i]) {
+            return fail(BMQCRC_EINVAL,
+                        "message " + std::to_string(i) + " lies outside [arena, arena+arena_bytes)");
+        }
     }
     return 0;
 }
@@ -333,32 +399,177 @@ int bmqcrc_crc32c_batch(const void* arena, uint64_t arena_bytes, const uint64_t*
         return fail(BMQCRC_EINVAL, "at most 2^32-1 messages per batch");
     }
     bmqcrc_opts o;
-    memset(&o, 0, sizeof(o));
-    o.device = -1;
-    if (opts) {
-        memcpy(&o, opts, std::min<size_t>(sizeof(o), opts->struct_size ? opts->struct_size
-                                                                        : sizeof(o)));
-    }
-    uint32_t seg = o.seg_bytes;
-    int rc = check_seg(&seg);
-    if (rc) {
+    uint32_t seg;
+    int dev, rc;
+    if ((rc = parse_opts(opts, &o, &seg, &dev))) {
         return rc;
     }
-    int dev;
-    if ((rc = resolve_device(o.device, &dev))) {
-        return rc;
-    }
-    if (!(o.flags & BMQCRC_F_DEVICE_PTRS)) {
-        // Host pointers: bounds check here (device arrays are trusted).
-        for (uint64_t i = 0; i < n; ++i) {
-            if (offsets[i] > arena_bytes || lengths[i] > arena_bytes - offsets[i]) {
-                return fail(BMQCRC_EINVAL, "message " + std::to_string(i) +
-                                               " lies outside [arena, arena+arena_bytes)");
-            }
-        }
+    if (!(o.flags & BMQCRC_F_DEVICE_PTRS) && (rc = check_ranges(offsets, lengths, n, arena_bytes))) {
+        return rc;  // device arrays are trusted
     }
     return batch_one(dev, o.stream, o.flags, seg, arena, arena_bytes, offsets, lengths, seeds,
                      out, n);
+}
+
+int bmqcrc_crc32c_verify(const void* arena, uint64_t arena_bytes, const uint64_t* offsets,
+                         const uint32_t* lengths, const uint32_t* expected, uint64_t n,
+                         uint64_t* n_bad, uint64_t* bad_idx, uint64_t bad_cap,
+                         const bmqcrc_opts* opts)
+{
+    t_err.clear();
+    if (!n_bad) {
+        return fail(BMQCRC_EINVAL, "n_bad is required");
+    }
+    *n_bad = 0;
+    if (n == 0) {
+        return 0;
+    }
+    if (!offsets || !lengths || !expected || (!arena && arena_bytes) || (bad_cap && !bad_idx)) {
+        return fail(BMQCRC_EINVAL, "null pointer argument");
+    }
+    if (n > 0xFFFFFFFFull) {
+        return fail(BMQCRC_EINVAL, "at most 2^32-1 messages per batch");
+    }
+    bmqcrc_opts o;
+    uint32_t seg;
+    int dev, rc;
+    if ((rc = parse_opts(opts, &o, &seg, &dev))) {
+        return rc;
+    }
+    const bool dev_ptrs = (o.flags & BMQCRC_F_DEVICE_PTRS) != 0;
+    if (!dev_ptrs && (rc = check_ranges(offsets, lengths, n, arena_bytes))) {
+        return rc;
+    }
+    Ctx c;
+    if ((rc = open_ctx(dev, o.stream, &c))) {
+        return rc;
+    }
+    Workspace* w = c.w;
+    std::lock_guard<std::mutex> g(w->mu);
+    const uint32_t cap = (uint32_t)std::min<uint64_t>(bad_cap, 1u << 24);
+    if ((rc = w->out.ensure(4 * n)) || (rc = w->vcount.ensure(4)) ||
+        (rc = w->vidx.ensure(4ull * std::max<uint32_t>(cap, 1)))) {
+        return rc;
+    }
+    const void* d_arena = arena;
+    const uint64_t* d_off = offsets;
+    const uint32_t* d_len = lengths;
+    const uint32_t* d_exp = expected;
+    if (!dev_ptrs) {
+        if ((rc = stage(c, w->arena, arena, arena_bytes)) ||
+            (rc = stage(c, w->offsets, offsets, 8 * n)) ||
+            (rc = stage(c, w->lengths, lengths, 4 * n)) ||
+            (rc = stage(c, w->expected, expected, 4 * n))) {
+            return rc;
+        }
+        d_arena = w->arena.p;
+        d_off = (const uint64_t*)w->offsets.p;
+        d_len = (const uint32_t*)w->lengths.p;
+        d_exp = (const uint32_t*)w->expected.p;
+    }
+    if ((rc = run_batch(c, o.flags, seg, d_arena, arena_bytes, d_off, d_len, nullptr,
+                        (uint32_t*)w->out.p, n))) {
+        return rc;
+    }
+    HIP_TRY(hipMemsetAsync(w->vcount.p, 0, 4, c.s));
+    if (bmqcrc_launch_compare((const uint32_t*)w->out.p, d_exp, n, (uint32_t*)w->vcount.p,
+                              (uint32_t*)w->vidx.p, cap, (void*)c.s)) {
+        return fail(BMQCRC_EIO, "compare launch failed");
+    }
+    uint32_t cnt = 0;
+    HIP_TRY(hipMemcpyAsync(&cnt, w->vcount.p, 4, hipMemcpyDeviceToHost, c.s));
+    HIP_TRY(hipStreamSynchronize(c.s));
+    *n_bad = cnt;
+    const uint32_t take = std::min(cnt, cap);
+    if (take) {
+        std::vector<uint32_t> idx(take);
+        HIP_TRY(hipMemcpy(idx.data(), w->vidx.p, 4ull * take, hipMemcpyDeviceToHost));
+        std::sort(idx.begin(), idx.end());
+        for (uint32_t k = 0; k < take; ++k) {
+            bad_idx[k] = idx[k];
+        }
+    }
+    return 0;
+}
+
+int bmqcrc_crc32c_blobs(const void* arena, uint64_t arena_bytes, const uint64_t* buf_offsets,
+                        const uint32_t* buf_lengths, uint64_t nbuf,
+                        const uint64_t* msg_first_buf, const uint32_t* seeds, uint32_t* out,
+                        uint64_t n, const bmqcrc_opts* opts)
+{
+    t_err.clear();
+    if (n == 0) {
+        return 0;
+    }
+    if (!msg_first_buf || !out || (nbuf && (!buf_offsets || !buf_lengths)) ||
+        (!arena && arena_bytes)) {
+        return fail(BMQCRC_EINVAL, "null pointer argument");
+    }
+    if (nbuf > 0xFFFFFFFFull || n > 0xFFFFFFFFull) {
+        return fail(BMQCRC_EINVAL, "at most 2^32-1 buffers and blobs per call");
+    }
+    bmqcrc_opts o;
+    uint32_t seg;
+    int dev, rc;
+    if ((rc = parse_opts(opts, &o, &seg, &dev))) {
+        return rc;
+    }
+    const bool dev_ptrs = (o.flags & BMQCRC_F_DEVICE_PTRS) != 0;
+    if (!dev_ptrs) {
+        if ((rc = check_ranges(buf_offsets, buf_lengths, nbuf, arena_bytes))) {
+            return rc;
+        }
+        for (uint64_t m = 0; m < n; ++m) {
+            if (msg_first_buf[m] > msg_first_buf[m + 1] || msg_first_buf[m + 1] > nbuf) {
+                return fail(BMQCRC_EINVAL, "msg_first_buf must be non-decreasing and <= nbuf");
+            }
+        }
+    }
+    Ctx c;
+    if ((rc = open_ctx(dev, o.stream, &c))) {
+        return rc;
+    }
+    Workspace* w = c.w;
+    std::lock_guard<std::mutex> g(w->mu);
+    if ((rc = w->buf_crc.ensure(4 * std::max<uint64_t>(nbuf, 1)))) {
+        return rc;
+    }
+    const void* d_arena = arena;
+    const uint64_t* d_off = buf_offsets;
+    const uint32_t* d_len = buf_lengths;
+    const uint64_t* d_first = msg_first_buf;
+    const uint32_t* d_seeds = seeds;
+    uint32_t* d_out = out;
+    if (!dev_ptrs) {
+        if ((rc = stage(c, w->arena, arena, arena_bytes)) ||
+            (rc = stage(c, w->offsets, buf_offsets, 8 * nbuf)) ||
+            (rc = stage(c, w->lengths, buf_lengths, 4 * nbuf)) ||
+            (rc = stage(c, w->first_buf, msg_first_buf, 8 * (n + 1))) ||
+            (seeds && (rc = stage(c, w->seeds, seeds, 4 * n))) || (rc = w->out.ensure(4 * n))) {
+            return rc;
+        }
+        d_arena = w->arena.p;
+        d_off = (const uint64_t*)w->offsets.p;
+        d_len = (const uint32_t*)w->lengths.p;
+        d_first = (const uint64_t*)w->first_buf.p;
+        d_seeds = seeds ? (const uint32_t*)w->seeds.p : nullptr;
+        d_out = (uint32_t*)w->out.p;
+    }
+    if (nbuf && (rc = run_batch(c, o.flags, seg, d_arena, arena_bytes, d_off, d_len, nullptr,
+                                (uint32_t*)w->buf_crc.p, nbuf))) {
+        return rc;
+    }
+    if (bmqcrc_launch_blob_combine((const uint32_t*)w->buf_crc.p, d_len, d_first, d_seeds, d_out,
+                                   n, (void*)c.s)) {
+        return fail(BMQCRC_EIO, "blob combine launch failed");
+    }
+    if (!dev_ptrs) {
+        HIP_TRY(hipMemcpyAsync(out, d_out, 4 * n, hipMemcpyDeviceToHost, c.s));
+        HIP_TRY(hipStreamSynchronize(c.s));
+    } else if (!(o.flags & BMQCRC_F_ASYNC)) {
+        HIP_TRY(hipStreamSynchronize(c.s));
+    }
+    return 0;
 }
 
 int bmqcrc_crc32c_batch_multi(const void* arena, uint64_t arena_bytes, const uint64_t* offsets,

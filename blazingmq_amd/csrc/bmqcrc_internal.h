@@ -58,7 +58,13 @@ struct BatchArgs {
 }  // namespace bmqcrc
 
 // Launchers (crc32c_kernels.hip).  All asynchronous on `stream`.
-extern "C" int bmqcrc_launch_batch(const bmqcrc::BatchArgs* a, void* stream, int num_cus,
+extern "C" __attribute__((visibility("hidden"))) int bmqcrc_launch_batch(const bmqcrc::BatchArgs* a, void* stream, int num_cus,
                                    void* ev_start, void* ev_stop);
-extern "C" int bmqcrc_launch_fill(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t begin,
+extern "C" __attribute__((visibility("hidden"))) int bmqcrc_launch_compare(const uint32_t* got, const uint32_t* expected, uint64_t n,
+                                     uint32_t* bad_count, uint32_t* bad_idx, uint32_t bad_cap,
+                                     void* stream);
+extern "C" __attribute__((visibility("hidden"))) int bmqcrc_launch_blob_combine(const uint32_t* buf_crc, const uint32_t* buf_len,
+                                         const uint64_t* msg_first_buf, const uint32_t* seeds,
+                                         uint32_t* out, uint64_t n, void* stream);
+extern "C" __attribute__((visibility("hidden"))) int bmqcrc_launch_fill(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t begin,
                                   void* stream);

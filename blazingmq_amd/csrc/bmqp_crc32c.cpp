@@ -3,6 +3,9 @@
 #include "bmqp_crc32c.h"
 
 #include <stdint.h>
+#include <string.h>
+
+#include <vector>
 
 namespace BloombergLP {
 namespace bmqp {
@@ -43,6 +46,41 @@ int Crc32c::calculateBatch(const void* arena,
     static_assert(sizeof(unsigned int) == sizeof(uint32_t), "u32");
     return bmqcrc_crc32c_batch(arena, arenaBytes, reinterpret_cast<const uint64_t*>(offsets),
                                lengths, seeds, crcs, count, opts);
+}
+
+int Crc32c::calculateBatch(const bdlbb::Blob* blobs,
+                           unsigned int       count,
+                           const unsigned int* seeds,
+                           unsigned int*      crcs,
+                           const bmqcrc_opts* opts)
+{
+    // Same buffer selection as calculate(const Blob&): every buffer but the
+    // last in full, the last up to lastDataBufferLength().
+    std::vector<uint64_t> off, first(1, 0);
+    std::vector<uint32_t> len;
+    uint64_t total = 0;
+    for (unsigned int b = 0; b < count; ++b) {
+        const int nb = blobs[b].numDataBuffers();
+        for (int i = 0; i < nb; ++i) {
+            const int n = (i + 1 < nb) ? blobs[b].buffer(i).size() : blobs[b].lastDataBufferLength();
+            off.push_back(total);
+            len.push_back(static_cast<uint32_t>(n));
+            total += static_cast<uint64_t>(n);
+        }
+        first.push_back(off.size());
+    }
+    std::vector<char> arena(total + 1);
+    size_t k = 0;
+    for (unsigned int b = 0; b < count; ++b) {
+        const int nb = blobs[b].numDataBuffers();
+        for (int i = 0; i < nb; ++i, ++k) {
+            if (len[k]) {
+                memcpy(&arena[off[k]], blobs[b].buffer(i).data(), len[k]);
+            }
+        }
+    }
+    return bmqcrc_crc32c_blobs(arena.data(), total, off.data(), len.data(), len.size(),
+                               first.data(), seeds, crcs, count, opts);
 }
 
 }  // namespace bmqp

@@ -30,6 +30,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "bmqcrc_internal.h"
 #include "crc32c_consts.h"
 
@@ -808,6 +810,61 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_scatter(BatchArgs a)
     }
 }
 
+// ------------------------------------------------- verify / blob combine
+// Mismatch detection for journal recovery: count and record indices
+// (unordered; the host sorts the short list).
+__global__ void k_compare(const uint32_t* got, const uint32_t* expected, uint64_t n,
+                          uint32_t* bad_count, uint32_t* bad_idx, uint32_t bad_cap)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        if (got[i] != expected[i]) {
+            const uint32_t slot = atomicAdd(bad_count, 1u);
+            if (slot < bad_cap) {
+                bad_idx[slot] = (uint32_t)i;
+            }
+        }
+    }
+}
+
+// Blob chaining (bmqp_crc32c.cpp:47-67): acc = seed; for each buffer j of
+// blob m: acc = calculate(buf_j, acc) = acc * x^(8 len_j) ^ crc0(buf_j).
+// x^e is applied with the 31 constant matrices (per-lane, no ballots: the
+// trip counts differ between lanes).
+__device__ uint32_t mul_xpow_lane(uint32_t v, uint32_t e)
+{
+    for (int j = 0; j < 31; ++j) {
+        if ((e >> j) & 1u) {
+            uint32_t a0 = 0, a1 = 0;
+#pragma unroll
+            for (int t = 0; t < 32; t += 2) {
+                a0 = xand(a0, bitmask(v, t), c_x2col[j][t]);
+                a1 = xand(a1, bitmask(v, t + 1), c_x2col[j][t + 1]);
+            }
+            v = a0 ^ a1;
+        }
+    }
+    return v;
+}
+
+__global__ void k_blob_combine(const uint32_t* buf_crc, const uint32_t* buf_len,
+                               const uint64_t* msg_first_buf, const uint32_t* seeds,
+                               uint32_t* out, uint64_t n)
+{
+    for (uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; m < n;
+         m += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t acc = seeds ? seeds[m] : 0u;
+        const uint64_t b1 = msg_first_buf[m + 1];
+        for (uint64_t b = msg_first_buf[m]; b < b1; ++b) {
+            const uint32_t len = buf_len[b];
+            if (len) {
+                acc = mul_xpow_lane(acc, mersenne31(8ull * len)) ^ buf_crc[b];
+            }
+        }
+        out[m] = acc;
+    }
+}
+
 // ------------------------------------------------------- synthetic payload
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x)
 {
@@ -870,6 +927,32 @@ extern "C" int bmqcrc_launch_batch(const BatchArgs* a, void* stream, int num_cus
     if (ev_stop) {
         (void)hipEventRecord((hipEvent_t)ev_stop, s);
     }
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" int bmqcrc_launch_compare(const uint32_t* got, const uint32_t* expected, uint64_t n,
+                                     uint32_t* bad_count, uint32_t* bad_idx, uint32_t bad_cap,
+                                     void* stream)
+{
+    if (n == 0) {
+        return 0;
+    }
+    const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_compare, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, got,
+                       expected, n, bad_count, bad_idx, bad_cap);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" int bmqcrc_launch_blob_combine(const uint32_t* buf_crc, const uint32_t* buf_len,
+                                         const uint64_t* msg_first_buf, const uint32_t* seeds,
+                                         uint32_t* out, uint64_t n, void* stream)
+{
+    if (n == 0) {
+        return 0;
+    }
+    const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_blob_combine, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                       buf_crc, buf_len, msg_first_buf, seeds, out, n);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

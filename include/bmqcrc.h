@@ -84,6 +84,28 @@ int bmqcrc_crc32c_batch(const void* arena, uint64_t arena_bytes, const uint64_t*
                         const uint32_t* lengths, const uint32_t* seeds, uint32_t* out,
                         uint64_t n, const bmqcrc_opts* opts);
 
+/* Batched verification (journal recovery, mqbs_filestore.cpp:2603-2624):
+ * computes the CRC of every message exactly like bmqcrc_crc32c_batch (seed 0)
+ * and compares it on the device with expected[i].  *n_bad receives the number
+ * of mismatches; the indices of up to bad_cap of them are written to bad_idx
+ * in ascending order (bad_idx may be NULL).  Pointer kinds follow opts->flags
+ * (n_bad/bad_idx are always host memory).  GPU only. */
+int bmqcrc_crc32c_verify(const void* arena, uint64_t arena_bytes, const uint64_t* offsets,
+                         const uint32_t* lengths, const uint32_t* expected, uint64_t n,
+                         uint64_t* n_bad, uint64_t* bad_idx, uint64_t bad_cap,
+                         const bmqcrc_opts* opts);
+
+/* bmqp::Crc32c::calculate(const bdlbb::Blob&, crc) (bmqp_crc32c.cpp:47-67) for
+ * n blobs at once.  Blob m is the concatenation of buffers
+ * [msg_first_buf[m], msg_first_buf[m+1]) of (buf_offsets, buf_lengths) in
+ * the arena (msg_first_buf has n+1 entries); out[m] = its CRC chained from
+ * seeds ? seeds[m] : 0.  Per-buffer CRCs are combined on the device with
+ * crc(A||B) = crc(A) * x^(8|B|) ^ crc0(B).  GPU only. */
+int bmqcrc_crc32c_blobs(const void* arena, uint64_t arena_bytes, const uint64_t* buf_offsets,
+                        const uint32_t* buf_lengths, uint64_t nbuf,
+                        const uint64_t* msg_first_buf, const uint32_t* seeds, uint32_t* out,
+                        uint64_t n, const bmqcrc_opts* opts);
+
 /* Host-pointer batch sharded over `ndev` devices: messages are split into
  * contiguous byte-balanced slices, one per device, each on its own stream,
  * with no inter-device communication.  devices==NULL means 0..ndev-1. */

@@ -47,6 +47,16 @@ struct Crc32c {
                               unsigned int* crcs,
                               unsigned long long count,
                               const bmqcrc_opts* opts = 0);
+
+    /// Batched Blob overload: `crcs[i] = calculate(blobs[i], seeds ? seeds[i] :
+    /// 0)` for `i < count`, computed on an MI355X (the blobs' buffers are
+    /// gathered into one staging arena, CRC'd per buffer and chained on the
+    /// device).  Returns 0 or a negative BMQCRC_E* code; no CPU fallback.
+    static int calculateBatch(const bdlbb::Blob* blobs,
+                              unsigned int       count,
+                              const unsigned int* seeds,
+                              unsigned int*      crcs,
+                              const bmqcrc_opts* opts = 0);
 };
 
 }  // namespace bmqp

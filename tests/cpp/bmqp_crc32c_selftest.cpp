@@ -244,6 +244,31 @@ static void gpu_batch()
     for (size_t i = 0; i < got.size(); ++i) {
         CHECK_EQ(got[i], exp[i]);
     }
+
+    // batched Blob overload vs the scalar Blob overload
+    std::mt19937 rng(99);
+    std::vector<std::string> store;
+    store.reserve(4096);
+    std::vector<Blob> blobs(300);
+    std::vector<unsigned> seeds(blobs.size()), bexp(blobs.size()), bgot(blobs.size());
+    for (size_t b = 0; b < blobs.size(); ++b) {
+        const int nb = (int)(rng() % 9);
+        for (int i = 0; i < nb; ++i) {
+            store.emplace_back(rng() % 5000, '\0');
+            for (auto& ch : store.back()) {
+                ch = (char)rng();
+            }
+            blobs[b].appendDataBuffer(BlobBuffer(&store.back()[0], (int)store.back().size()));
+        }
+        seeds[b] = (rng() & 1) ? rng() : 0;
+        bexp[b] = Crc32c::calculate(blobs[b], seeds[b]);
+    }
+    CHECK_EQ(Crc32c::calculateBatch(blobs.data(), (unsigned)blobs.size(), seeds.data(),
+                                    bgot.data()),
+             0);
+    for (size_t b = 0; b < blobs.size(); ++b) {
+        CHECK_EQ(bgot[b], bexp[b]);
+    }
 }
 
 int main(int argc, char** argv)

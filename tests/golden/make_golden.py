@@ -12,7 +12,7 @@ Sources (all in /root/reference, read as text):
       test7/8 blob "one"+"two"+"three" -> 0xA0EA6901         (:845, :970)
       test7/8 277-byte sentence + 550 '#' -> 0xD86F726E      (:854-881, :980-1022)
   * src/applications/bmqstoragetool/integration-tests/data/test.bmq_data
-      (copied verbatim as test.bmq_data) with the journal CRC printed by
+      and test.bmq_journal (copied verbatim) with the journal CRC printed by
       bmqstoragetool in detail_result.txt:15,53 (3381945770) for the two
       MESSAGE records at DATA offsets 40 and 64 (payload_dump.txt).
   * RFC 3720 section B.4 (iSCSI CRC32C test patterns) as external known answers.
@@ -96,6 +96,15 @@ def main():
     crcs = [int(x) for x in re.findall(r"Crc32c\s*:\s*(\d+)", detail)]
     assert crcs == [3381945770, 3381945770], crcs
     shutil.copyfile(os.path.join(DATA_DIR, "test.bmq_data"), os.path.join(HERE, "test.bmq_data"))
+    shutil.copyfile(os.path.join(DATA_DIR, "test.bmq_journal"),
+                    os.path.join(HERE, "test.bmq_journal"))
+    # journal offsets of the two MESSAGE records as printed by bmqstoragetool
+    blocks = detail.split("RecordType      : ")
+    msg_offsets = [int(re.search(r"Offset\s*:\s*(\d+)", b).group(1)) for b in blocks
+                   if b.startswith("MESSAGE")]
+    assert msg_offsets == [224, 644], msg_offsets
+    out["journal_file"] = {"file": "test.bmq_journal", "message_record_offsets": msg_offsets,
+                           "crc": crcs}
     out["data_file"] = {
         "file": "test.bmq_data",
         "records": [{"record_offset": 40, "header_bytes": 12, "app_data_len": 11, "crc": crcs[0]},

@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 
 def _dev_batch(cuda, arena_np, offs, lens, seeds=None, seg_bytes=0):
     import torch
-    arena = torch.from_numpy(np.ascontiguousarray(arena_np, dtype=np.uint8)).to(cuda)
+    arena = torch.from_numpy(np.array(arena_np, dtype=np.uint8, copy=True)).to(cuda)
     o = torch.tensor(np.asarray(offs, dtype=np.int64), device=cuda)
     ln = torch.tensor(np.asarray(lens, dtype=np.uint32).view(np.int32), device=cuda)
     sd = None
