@@ -78,6 +78,9 @@ __device__ __forceinline__ uint32_t mul_y(uint32_t v)
 // (scalar loads); bits no lane needs are skipped wave-uniformly.
 __device__ uint32_t mul_xpow(uint32_t v, uint32_t e)
 {
+    if (__ballot(e != 0) == 0) {
+        return v;
+    }
     for (int j = 0; j < 31; ++j) {
         const bool bit = (e >> j) & 1u;
         if (__ballot(bit) == 0) {
@@ -348,6 +351,48 @@ __device__ __forceinline__ SegGeom seg_geom(uint64_t mstart, uint32_t len, uint3
     return g;
 }
 
+// Segment -> (message, part) for the fold kernel, by planner mode.
+struct SegRef {
+    uint32_t msg, k;
+};
+
+struct SegDesc {
+    uint64_t off;
+    uint32_t msg, k, len, seed;
+};
+
+__device__ __forceinline__ SegRef map_segment(const BatchArgs& a, uint32_t seg, bool valid,
+                                              uint32_t identity, uint32_t uni, uint32_t sorted)
+{
+    SegRef r = {0u, 0u};
+    if (valid) {
+        if (identity) {
+            r.msg = seg;
+        } else if (uni) {
+            r.msg = seg / uni;
+            r.k = seg - r.msg * uni;
+        } else if (sorted) {
+            r.msg = a.seginfo[2u * seg];
+            r.k = a.seginfo[2u * seg + 1u];
+        } else {
+            r.msg = seg < a.max_segs ? a.seg2msg[seg] : find_msg(a, seg);
+            r.k = seg - seg_first_g(a, r.msg);
+        }
+    }
+    return r;
+}
+
+__device__ __forceinline__ SegDesc fetch_desc(const BatchArgs& a, SegRef r, bool valid)
+{
+    SegDesc d = {0ull, r.msg, r.k, 0u, 0u};
+    if (valid) {
+        d.off = a.offsets[r.msg];
+        d.len = a.lengths[r.msg];
+        d.seed = a.seeds ? a.seeds[r.msg] : 0u;
+    }
+    return d;
+}
+
 template <bool NT>
 __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
 {
@@ -375,31 +420,37 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
 
     const uint32_t rd_off = (uint32_t)lane * 128u + (((uint32_t)lane >> 1) & 7u) * 16u;
 
-    for (uint32_t g = blockIdx.x * kWavesPerBlock + wave; g < ngroups;
-         g += gridDim.x * kWavesPerBlock) {
+    const uint32_t stride = gridDim.x * kWavesPerBlock;
+    const uint32_t seg_shift = (SEG & (SEG - 1u)) == 0 ? (uint32_t)__builtin_ctz(SEG) : 0u;
+    // Descriptor pipeline across groups: the (message, part) of the group
+    // after next and the (offset, length, seed) of the next group are loaded
+    // while the current group folds, so no group starts on a cold load.
+    uint32_t g = blockIdx.x * kWavesPerBlock + wave;
+    SegDesc nxt = {0ull, 0u, 0u, 0u, 0u};
+    SegRef ref2 = {0u, 0u};
+    if (g < ngroups) {
+        const uint32_t s0 = g * 64u + (uint32_t)lane;
+        nxt = fetch_desc(a, map_segment(a, s0, s0 < total, identity, uni, sorted), s0 < total);
+        const uint32_t s1 = (g + stride) * 64u + (uint32_t)lane;
+        ref2 = map_segment(a, s1, g + stride < ngroups && s1 < total, identity, uni, sorted);
+    }
+    for (; g < ngroups; g += stride) {
         // ---------------------------------------------------- descriptor
         const uint32_t seg = g * 64u + (uint32_t)lane;
         const bool valid = seg < total;
-        uint32_t msg = 0, len = 0, seed = 0, k = 0;
-        uint64_t off = 0;
-        if (valid) {
-            if (identity) {
-                msg = seg;
-            } else if (uni) {
-                msg = seg / uni;
-                k = seg - msg * uni;
-            } else if (sorted) {
-                msg = a.seginfo[2u * seg];
-                k = a.seginfo[2u * seg + 1u];
-            } else {
-                msg = seg < a.max_segs ? a.seg2msg[seg] : find_msg(a, seg);
-                k = seg - seg_first_g(a, msg);
-            }
-            off = a.offsets[msg];
-            len = a.lengths[msg];
-            seed = a.seeds ? a.seeds[msg] : 0u;
+        const SegDesc cur = nxt;
+        {
+            const uint32_t s1 = (g + stride) * 64u + (uint32_t)lane;
+            const bool v1 = g + stride < ngroups && s1 < total;
+            nxt = fetch_desc(a, ref2, v1);
+            const uint32_t s2 = (g + 2u * stride) * 64u + (uint32_t)lane;
+            ref2 = map_segment(a, s2, g + 2u * stride < ngroups && s2 < total, identity, uni,
+                               sorted);
         }
-        const uint32_t nseg = valid ? (len - 1u) / SEG + 1u : 0u;
+        const uint32_t msg = cur.msg, k = cur.k, len = cur.len, seed = cur.seed;
+        const uint64_t off = cur.off;
+        const uint32_t nseg =
+            valid ? (seg_shift ? ((len - 1u) >> seg_shift) : (len - 1u) / SEG) + 1u : 0u;
         const uint64_t mstart = arena + off;
         const uint64_t mend = mstart + len;
         const SegGeom geo = seg_geom(mstart, len, k, nseg, SEG);
@@ -457,12 +508,16 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
                 dma_round<NT>(slot, dbase, dlim, dummy, r + 2);
             }
             const uint64_t p0 = L0 + ((uint64_t)r << 7);
-            if (r < nl && (p0 < inj_end || p0 + 128u > E)) {
+            const bool cut = r < nl && (p0 < S || p0 + 128u > E);  // bytes outside [S, E)
+            const bool inj = r < nl && p0 < inj_end && S < p0 + 128u;  // seed word here
+            if (cut || (inj && S != p0)) {
                 const int64_t sr = (int64_t)(S - p0);
                 const int64_t er = (int64_t)(E - p0);
                 const int sR = (int)(sr < -8 ? -8 : (sr > 136 ? 136 : sr));
                 const int eR = (int)(er < -8 ? -8 : (er > 136 ? 136 : er));
                 mask_round(m, sR, eR, first, c0);
+            } else if (inj) {
+                m[0] ^= c0;  // line-aligned message start: the seed is word 0
             }
             if (r + 1 < nl) {
                 fold_round(q, m);
@@ -477,8 +532,10 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         // message end with x^(8 after) (sparse exponent: bits no lane needs are
         // skipped wave-uniformly).
         uint32_t contrib = 0;
-        if (valid) {
-            const uint32_t padE = (uint32_t)(L0 + ((uint64_t)nl << 7) - E);
+        const uint32_t padE = valid ? (uint32_t)(L0 + ((uint64_t)nl << 7) - E) : 0u;
+        if (__ballot(padE != 0) == 0) {
+            contrib = valid ? crc : 0u;
+        } else if (valid) {
             contrib = gmul(crc, c_xneg8[padE]);
         }
         const uint32_t e_after = valid ? mersenne31(8ull * (mend - E)) : 0u;
