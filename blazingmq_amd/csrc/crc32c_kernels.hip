@@ -745,13 +745,50 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_emit(BatchArgs a)
         hist[threadIdx.x] = 0;
     }
     __syncthreads();
+    // Windowed search: the 1024 segments of a tile belong to a short run of
+    // consecutive messages, so one global binary search per tile (thread 0)
+    // plus a 1025-entry window of the prefix in LDS replaces a 22-step
+    // dependent global search per segment.
+    __shared__ uint32_t win[kPlanBlock + 1];
+    __shared__ uint32_t win_lo;
     const uint64_t lo = (uint64_t)blockIdx.x * a.per_seg;
     const uint64_t hi = min(lo + a.per_seg, lim);
-    for (uint64_t g = lo + threadIdx.x; g < hi; g += kPlanBlock) {
-        const uint32_t msg = find_msg(a, (uint32_t)g);
-        const uint32_t k = (uint32_t)g - seg_first_g(a, msg);
-        a.seg2msg[g] = msg;
-        atomicAdd(&hist[seg_class(a, msg, k)], 1u);
+    if (threadIdx.x == 0 && lo < hi) {
+        win_lo = find_msg(a, (uint32_t)lo);  // later tiles start where the last one ended
+    }
+    __syncthreads();
+    for (uint64_t base = lo; base < hi; base += kPlanBlock) {
+        const uint64_t m0 = win_lo;
+        win[threadIdx.x] = (m0 + threadIdx.x < a.n) ? seg_first_g(a, m0 + threadIdx.x) : 0xffffffffu;
+        if (threadIdx.x == 0) {
+            win[kPlanBlock] = (m0 + kPlanBlock < a.n) ? seg_first_g(a, m0 + kPlanBlock) : 0xffffffffu;
+        }
+        __syncthreads();
+        const uint64_t g = base + threadIdx.x;
+        if (g < hi) {
+            uint32_t msg;
+            if ((uint32_t)g < win[kPlanBlock]) {
+                uint32_t l = 0, h = kPlanBlock;  // win[l] <= g < win[h]
+                while (h - l > 1) {
+                    const uint32_t mid = (l + h) >> 1;
+                    if (win[mid] <= (uint32_t)g) {
+                        l = mid;
+                    } else {
+                        h = mid;
+                    }
+                }
+                msg = (uint32_t)m0 + l;
+            } else {
+                msg = find_msg(a, (uint32_t)g);  // window exhausted (empty messages)
+            }
+            const uint32_t k = (uint32_t)g - seg_first_g(a, msg);
+            a.seg2msg[g] = msg;
+            atomicAdd(&hist[seg_class(a, msg, k)], 1u);
+            if (g + 1 == min(base + kPlanBlock, hi)) {
+                win_lo = msg;  // message of the tile's last segment starts the next window
+            }
+        }
+        __syncthreads();
     }
     __syncthreads();
     if (threadIdx.x == 0) {
