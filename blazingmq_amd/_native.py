@@ -78,11 +78,36 @@ lib.bmqcrc_last_error.argtypes = []
 lib.bmqcrc_version.restype = _u32
 lib.bmqcrc_version.argtypes = []
 
+# include/bmqcrc_protocol.h
+_i64, _pu64, _pint, _popts = ctypes.c_int64, ctypes.POINTER(_u64), ctypes.POINTER(_int), \
+    ctypes.POINTER(Opts)
+lib.bmqcrc_put_event_scan.restype = _i64
+lib.bmqcrc_put_event_scan.argtypes = [_vp, _u64, _vp, _vp, _vp, _u64]
+lib.bmqcrc_put_event_fill_crcs.restype = _i64
+lib.bmqcrc_put_event_fill_crcs.argtypes = [_vp, _u64, _popts]
+lib.bmqcrc_put_event_verify.restype = _int
+lib.bmqcrc_put_event_verify.argtypes = [_vp, _u64, _pu64, _pu64, _vp, _u64, _popts]
+lib.bmqcrc_journal_scan.restype = _i64
+lib.bmqcrc_journal_scan.argtypes = [_vp, _u64, _vp, _u64, _vp, _vp, _vp, _vp, _u64]
+lib.bmqcrc_recover_verify.restype = _int
+lib.bmqcrc_recover_verify.argtypes = [_vp, _u64, _vp, _u64, _pu64, _pu64, _vp, _u64, _popts]
+lib.bmqcrc_csl_scan.restype = _i64
+lib.bmqcrc_csl_scan.argtypes = [_vp, _u64, _vp, _vp, _vp, _vp, _u64, _pint, _pu64]
+lib.bmqcrc_csl_validate.restype = _int
+lib.bmqcrc_csl_validate.argtypes = [_vp, _u64, _vp, _pint, _pu64, _pu64, _popts]
+
 
 def check(rc):
     if rc != BMQCRC_OK:
         raise BmqCrcError(rc, lib.bmqcrc_last_error().decode(errors="replace"))
     return rc
+
+
+def check_count(n):
+    """Scans return a count (>= 0) or a negative BMQCRC_E* code."""
+    if n < 0:
+        raise BmqCrcError(n, lib.bmqcrc_last_error().decode(errors="replace"))
+    return n
 
 
 def make_opts(device=-1, stream=None, flags=0, seg_bytes=0):

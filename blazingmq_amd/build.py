@@ -20,7 +20,8 @@ ORACLE = os.path.join(ROOT, "oracle")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-PRODUCT_SOURCES = ["crc32c_kernels.hip", "bmqcrc_host.cpp", "crc32c_cpu.cpp", "bmqp_crc32c.cpp"]
+PRODUCT_SOURCES = ["crc32c_kernels.hip", "bmqcrc_host.cpp", "crc32c_cpu.cpp", "bmqp_crc32c.cpp",
+                   "bmqcrc_protocol.cpp"]
 PRODUCT_DEPS = ["bmqcrc_internal.h", "crc32c_consts.h"]
 
 
@@ -49,7 +50,8 @@ def build_product(force=False):
     target = os.path.join(LIB, "libbmqcrc.so")
     srcs = [os.path.join(CSRC, s) for s in PRODUCT_SOURCES]
     deps = srcs + [os.path.join(CSRC, d) for d in PRODUCT_DEPS] + [
-        os.path.join(ROOT, "include", "bmqcrc.h"), os.path.join(ROOT, "include", "bmqp_crc32c.h")]
+        os.path.join(ROOT, "include", "bmqcrc.h"), os.path.join(ROOT, "include", "bmqp_crc32c.h"),
+        os.path.join(ROOT, "include", "bmqcrc_protocol.h")]
     if force or _stale(target, deps):
         objs = []
         for s in srcs:

@@ -84,7 +84,7 @@ struct Workspace {
     // host-pointer staging
     DevBuf arena, offsets, lengths, seeds, out;
     // verify / blobs
-    DevBuf expected, vcount, vidx, buf_crc, first_buf;
+    DevBuf expected, vcount, vidx, vblock, buf_crc, first_buf;
     // BMQCRC_F_TIME_KERNEL: event pairs around k_fold not yet reported
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timing, spare;
     ~Workspace()
@@ -362,6 +362,16 @@ int check_ranges(const uint64_t* offsets, const uint32_t* lengths, uint64_t n,
 
 }  // namespace
 
+extern "C" int bmqcrc_set_error(int rc, const char* msg)
+{
+    return fail(rc, msg ? msg : "");
+}
+
+extern "C" void bmqcrc_clear_error(void)
+{
+    t_err.clear();
+}
+
 extern "C" {
 
 uint32_t bmqcrc_crc32c(const void* data, uint32_t length, uint32_t crc)
@@ -481,9 +491,38 @@ int bmqcrc_crc32c_verify(const void* arena, uint64_t arena_bytes, const uint64_t
     HIP_TRY(hipStreamSynchronize(c.s));
     *n_bad = cnt;
     const uint32_t take = std::min(cnt, cap);
+    if (take && cnt > cap) {
+        // more mismatches than slots: the single pass kept an arbitrary
+        // subset, so rebuild the list in index order (lowest `cap` indices)
+        const uint32_t nb = (uint32_t)std::min<uint64_t>((n + 255) / 256, 4096);
+        if ((rc = w->vblock.ensure(4ull * nb))) {
+            return rc;
+        }
+        uint32_t* d_blk = (uint32_t*)w->vblock.p;
+        if (bmqcrc_launch_compare_ordered((const uint32_t*)w->out.p, d_exp, n, d_blk, nb,
+                                          nullptr, cap, 0, (void*)c.s)) {
+            return fail(BMQCRC_EIO, "ordered compare launch failed");
+        }
+        std::vector<uint32_t> blk(nb);
+        HIP_TRY(hipMemcpyAsync(blk.data(), d_blk, 4ull * nb, hipMemcpyDeviceToHost, c.s));
+        HIP_TRY(hipStreamSynchronize(c.s));
+        uint64_t run = 0;
+        for (uint32_t b = 0; b < nb; ++b) {
+            const uint32_t k = blk[b];
+            blk[b] = (uint32_t)std::min<uint64_t>(run, 0xFFFFFFFFu);
+            run += k;
+        }
+        HIP_TRY(hipMemcpyAsync(d_blk, blk.data(), 4ull * nb, hipMemcpyHostToDevice, c.s));
+        if (bmqcrc_launch_compare_ordered((const uint32_t*)w->out.p, d_exp, n, d_blk, nb,
+                                          (uint32_t*)w->vidx.p, cap, 1, (void*)c.s)) {
+            return fail(BMQCRC_EIO, "ordered compare launch failed");
+        }
+        HIP_TRY(hipStreamSynchronize(c.s));  // blk is read by the async H2D copy
+    }
     if (take) {
         std::vector<uint32_t> idx(take);
-        HIP_TRY(hipMemcpy(idx.data(), w->vidx.p, 4ull * take, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpyAsync(idx.data(), w->vidx.p, 4ull * take, hipMemcpyDeviceToHost, c.s));
+        HIP_TRY(hipStreamSynchronize(c.s));
         std::sort(idx.begin(), idx.end());
         for (uint32_t k = 0; k < take; ++k) {
             bad_idx[k] = idx[k];

@@ -68,3 +68,13 @@ extern "C" __attribute__((visibility("hidden"))) int bmqcrc_launch_blob_combine(
                                          uint32_t* out, uint64_t n, void* stream);
 extern "C" __attribute__((visibility("hidden"))) int bmqcrc_launch_fill(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t begin,
                                   void* stream);
+// Ordered mismatch list: pass 0 writes per-block counts to block_cnt, pass 1
+// reads the exclusive prefix from block_cnt and writes the bad_cap lowest
+// mismatching indices to bad_idx (ascending).
+extern "C" __attribute__((visibility("hidden"))) int bmqcrc_launch_compare_ordered(const uint32_t* got, const uint32_t* expected,
+                                            uint64_t n, uint32_t* block_cnt, uint32_t nblocks,
+                                            uint32_t* bad_idx, uint32_t bad_cap, int pass,
+                                            void* stream);
+// Thread-local error message shared by every C-ABI source (bmqcrc_last_error).
+extern "C" __attribute__((visibility("hidden"))) int bmqcrc_set_error(int rc, const char* msg);
+extern "C" __attribute__((visibility("hidden"))) void bmqcrc_clear_error(void);

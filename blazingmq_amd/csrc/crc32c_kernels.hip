@@ -921,6 +921,58 @@ __global__ void k_compare(const uint32_t* got, const uint32_t* expected, uint64_
     }
 }
 
+// Ordered mismatch list, used when more messages mismatch than the caller's
+// bad_cap: block b owns indices [b*chunk, (b+1)*chunk); pass 1 counts its
+// mismatches, the host scans the counts, pass 2 writes each mismatch at its
+// global rank so the list holds exactly the bad_cap LOWEST indices (the
+// reference's walks stop at / report the first corrupt record).
+__global__ void k_compare_count(const uint32_t* got, const uint32_t* expected, uint64_t n,
+                                uint64_t chunk, uint32_t* block_cnt)
+{
+    const uint64_t lo = (uint64_t)blockIdx.x * chunk;
+    const uint64_t hi = min(n, lo + chunk);
+    uint32_t cnt = 0;
+    for (uint64_t base = lo; base < hi; base += blockDim.x) {
+        const uint64_t i = base + threadIdx.x;
+        cnt += __syncthreads_count(i < hi && got[i] != expected[i]);
+    }
+    if (threadIdx.x == 0) {
+        block_cnt[blockIdx.x] = cnt;
+    }
+}
+
+__global__ void k_compare_emit(const uint32_t* got, const uint32_t* expected, uint64_t n,
+                               uint64_t chunk, const uint32_t* block_off, uint32_t* bad_idx,
+                               uint32_t bad_cap)
+{
+    __shared__ uint32_t wave_cnt[16];
+    const uint64_t lo = (uint64_t)blockIdx.x * chunk;
+    const uint64_t hi = min(n, lo + chunk);
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t nwaves = blockDim.x >> 6;
+    uint32_t run = block_off[blockIdx.x];
+    for (uint64_t base = lo; base < hi && run < bad_cap; base += blockDim.x) {
+        const uint64_t i = base + threadIdx.x;
+        const bool bad = i < hi && got[i] != expected[i];
+        const uint64_t m = __ballot(bad);
+        const uint32_t below = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        if (lane == 0) {
+            wave_cnt[wave] = (uint32_t)__popcll(m);
+        }
+        __syncthreads();
+        uint32_t before = run, total = 0;
+        for (uint32_t w = 0; w < nwaves; ++w) {
+            before += (w < wave) ? wave_cnt[w] : 0u;
+            total += wave_cnt[w];
+        }
+        if (bad && before + below < bad_cap) {
+            bad_idx[before + below] = (uint32_t)i;
+        }
+        run += total;
+        __syncthreads();
+    }
+}
+
 // Blob chaining (bmqp_crc32c.cpp:47-67): acc = seed; for each buffer j of
 // blob m: acc = calculate(buf_j, acc) = acc * x^(8 len_j) ^ crc0(buf_j).
 // x^e is applied with the 31 constant matrices (per-lane, no ballots: the
@@ -1034,6 +1086,25 @@ extern "C" int bmqcrc_launch_compare(const uint32_t* got, const uint32_t* expect
     const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 4096);
     hipLaunchKernelGGL(k_compare, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, got,
                        expected, n, bad_count, bad_idx, bad_cap);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" int bmqcrc_launch_compare_ordered(const uint32_t* got, const uint32_t* expected,
+                                            uint64_t n, uint32_t* block_cnt, uint32_t nblocks,
+                                            uint32_t* bad_idx, uint32_t bad_cap, int pass,
+                                            void* stream)
+{
+    if (n == 0 || nblocks == 0) {
+        return 0;
+    }
+    const uint64_t chunk = (n + nblocks - 1) / nblocks;
+    if (pass == 0) {
+        hipLaunchKernelGGL(k_compare_count, dim3(nblocks), dim3(256), 0, (hipStream_t)stream,
+                           got, expected, n, chunk, block_cnt);
+    } else {
+        hipLaunchKernelGGL(k_compare_emit, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, got,
+                           expected, n, chunk, block_cnt, bad_idx, bad_cap);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -18,10 +18,16 @@ The reference computes ``Crc32c::calculate(appData)`` once per message inside
 ``packMessage`` (bmqp_puteventbuilder.cpp:302,320,400,413) and writes it into
 ``PutHeader::d_crc32c`` (:146-153).  ``PutEventBuilder(defer_crc=True)`` packs
 every message with the CRC field pending and ``finalize()`` fills all of them
-with one batched GPU call before the event is posted.
+with one batched GPU call before the event is posted
+(``bmqcrc_put_event_fill_crcs``: a native walk of the event, then one batch).
+``PutMessageIterator.verify_crcs()`` is the batched form of the iterator's
+recompute (bmqp_putmessageiterator.cpp:670-679): ``bmqcrc_put_event_verify``.
 """
+import ctypes
+
 import numpy as np
 
+from . import _native as N
 from .crc32c import Crc32c
 
 EVENT_HEADER_SIZE = 8
@@ -87,12 +93,12 @@ class PutEventBuilder:
         ev[4] = (PROTOCOL_VERSION << 6) | EVENT_TYPE_PUT
         ev[5] = EVENT_HEADER_SIZE // WORD
         if self.defer_crc and self._app_off:
-            crcs = Crc32c.calculate_batch(ev, np.asarray(self._app_off, np.uint64),
-                                          np.asarray(self._app_len, np.uint32))
-            pos = np.asarray(self._crc_pos, dtype=np.int64)
-            be = crcs.astype(">u4").view(np.uint8).reshape(-1, 4)
-            for k in range(4):
-                ev[pos + k] = be[:, k]
+            opts = N.make_opts()
+            n = N.check_count(N.lib.bmqcrc_put_event_fill_crcs(
+                ctypes.c_void_p(ev.ctypes.data), ev.size, ctypes.byref(opts)))
+            if n != len(self._app_off):
+                raise RuntimeError("PUT event walk found %d messages, packed %d"
+                                   % (n, len(self._app_off)))
         self._finalized = True
         return ev
 
@@ -107,6 +113,32 @@ class PutMessageIterator:
         if length != self.ev.size or (int(self.ev[4]) & 0x3F) != EVENT_TYPE_PUT:
             raise ValueError("not a PUT event of matching length")
         self.header_size = int(self.ev[5]) * WORD
+
+    def scan(self):
+        """Native walk (``bmqcrc_put_event_scan``, CPU only): numpy arrays
+        (app_offset, app_length, crc_pos) of every message."""
+        ev = np.ascontiguousarray(self.ev)
+        p = ctypes.c_void_p(ev.ctypes.data)
+        n = N.check_count(N.lib.bmqcrc_put_event_scan(p, ev.size, None, None, None, 0))
+        off, ln, pos = np.zeros(n, np.uint64), np.zeros(n, np.uint32), np.zeros(n, np.uint64)
+        if n:
+            N.check_count(N.lib.bmqcrc_put_event_scan(
+                p, ev.size, ctypes.c_void_p(off.ctypes.data), ctypes.c_void_p(ln.ctypes.data),
+                ctypes.c_void_p(pos.ctypes.data), n))
+        return off, ln, pos
+
+    def verify_crcs(self, bad_cap=1 << 16, device=-1):
+        """Check every PutHeader CRC against its application data in one GPU
+        batch.  Returns (n_messages, n_bad, bad message indices)."""
+        ev = np.ascontiguousarray(self.ev)
+        n_msgs, n_bad = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        bad = np.zeros(max(int(bad_cap), 1), np.uint64)
+        opts = N.make_opts(device=device)
+        N.check(N.lib.bmqcrc_put_event_verify(
+            ctypes.c_void_p(ev.ctypes.data), ev.size, ctypes.byref(n_msgs), ctypes.byref(n_bad),
+            ctypes.c_void_p(bad.ctypes.data), int(bad_cap), ctypes.byref(opts)))
+        k = min(int(n_bad.value), int(bad_cap))
+        return int(n_msgs.value), int(n_bad.value), bad[:k].copy()
 
     def __iter__(self):
         pos = self.header_size

@@ -4,8 +4,13 @@ Host-side mirror of the CRC part of ``mqbs::FileStore::recoverMessages``
 (/root/reference/src/groups/mqb/mqbs/mqbs_filestore.cpp:1045, record walk
 :1490, DATA checks :2495-2575, CRC check :2603-2624).  The reference walks the
 journal and CRCs one message at a time; here every MESSAGE record is
-collected first, then all payloads are verified with ONE batched GPU call
-(``bmqcrc_crc32c_verify``).
+collected first, then all payloads are verified with ONE batched GPU call.
+
+The product path is native: ``scan_partition`` / ``verify_partition`` call
+``bmqcrc_journal_scan`` / ``bmqcrc_recover_verify`` (include/bmqcrc_protocol.h,
+csrc/bmqcrc_protocol.cpp).  ``journal_message_records`` / ``data_app_ranges``
+restate the same walk in numpy; the CPU tests hold the two against each other
+and against the bmqstoragetool fixture.
 
 On-disk layouts (mqbs_filestoreprotocol.h):
   FileHeader (:306)        magic1 "!bmq", magic2 "BMQ!", PV(2b)|HW(6b), B(1b)|FileType(7b),
@@ -21,8 +26,11 @@ On-disk layouts (mqbs_filestoreprotocol.h):
   bytes, each equal to the padding count (bmqp_protocolutil.cpp:44, dword
   padding); MessageOffsetDwords counts 8-byte units.
 """
+import ctypes
+
 import numpy as np
 
+from . import _native as N
 from .crc32c import Crc32c
 
 MAGIC1 = 0x21626D71  # !bmq
@@ -124,20 +132,59 @@ def data_app_ranges(data, data_offsets):
     return app_off, app_len
 
 
-def verify_partition(journal, data, bad_cap=1 << 20):
-    """Recovery CRC check of a whole partition in one GPU batch.
+def _native_call(fn, *args):
+    try:
+        return fn(*args)
+    except N.BmqCrcError as e:
+        if e.rc == N.BMQCRC_EINVAL:
+            raise StorageFormatError(str(e)) from e
+        raise
 
-    Returns dict(n_messages, n_bad, bad_record_offsets, records).  A mismatch
-    is what the reference reports with BMQTSK_ALARMLOG_ALARM("RECOVERY")
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a.size else None
+
+
+def scan_partition(journal, data):
+    """Native walk (``bmqcrc_journal_scan``, CPU only): every MESSAGE record
+    as numpy arrays (record_offset, app_offset, app_length, crc32c)."""
+    j, d = np.ascontiguousarray(_as_u8(journal)), np.ascontiguousarray(_as_u8(data))
+
+    def scan(cap, *arrs):
+        n = N.lib.bmqcrc_journal_scan(_ptr(j), j.size, _ptr(d), d.size,
+                                      *[_ptr(a) if a is not None else None for a in arrs], cap)
+        return N.check_count(n)
+
+    n = _native_call(scan, 0, None, None, None, None)
+    out = {"record_offset": np.zeros(n, np.uint64), "app_offset": np.zeros(n, np.uint64),
+           "app_length": np.zeros(n, np.uint32), "crc32c": np.zeros(n, np.uint32)}
+    _native_call(scan, n, out["record_offset"], out["app_offset"], out["app_length"],
+                 out["crc32c"])
+    return out
+
+
+def verify_partition(journal, data, bad_cap=1 << 20, device=-1):
+    """Recovery CRC check of a whole partition: one native walk, one batched
+    GPU verify (``bmqcrc_recover_verify``).
+
+    Returns dict(n_messages, n_bad, bad_record_offsets).  A mismatch is what
+    the reference reports with BMQTSK_ALARMLOG_ALARM("RECOVERY")
     (mqbs_filestore.cpp:2613-2624); like the reference, recovery continues.
     """
-    recs = journal_message_records(journal)
-    d = _as_u8(data)
-    app_off, app_len = data_app_ranges(d, recs["data_offset"])
-    n_bad, bad_idx = Crc32c.verify_batch(d, app_off, app_len, recs["crc32c"], bad_cap=bad_cap)
-    return {"n_messages": int(app_off.size), "n_bad": n_bad,
-            "bad_record_offsets": recs["record_offset"][bad_idx], "bad_index": bad_idx,
-            "records": recs, "app_offset": app_off, "app_length": app_len}
+    j, d = np.ascontiguousarray(_as_u8(journal)), np.ascontiguousarray(_as_u8(data))
+    n_msgs, n_bad = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    bad = np.zeros(max(int(bad_cap), 1), np.uint64)
+    opts = N.make_opts(device=device)
+
+    def run():
+        return N.check(N.lib.bmqcrc_recover_verify(
+            _ptr(j), j.size, _ptr(d), d.size, ctypes.byref(n_msgs), ctypes.byref(n_bad),
+            _ptr(bad), int(bad_cap), ctypes.byref(opts)))
+
+    _native_call(run)
+    k = min(int(n_bad.value), int(bad_cap))
+    return {"n_messages": int(n_msgs.value), "n_bad": int(n_bad.value),
+            "bad_record_offsets": bad[:k].copy()}
 
 
 # ----------------------------------------------------------------------------

@@ -87,8 +87,8 @@ int bmqcrc_crc32c_batch(const void* arena, uint64_t arena_bytes, const uint64_t*
 /* Batched verification (journal recovery, mqbs_filestore.cpp:2603-2624):
  * computes the CRC of every message exactly like bmqcrc_crc32c_batch (seed 0)
  * and compares it on the device with expected[i].  *n_bad receives the number
- * of mismatches; the indices of up to bad_cap of them are written to bad_idx
- * in ascending order (bad_idx may be NULL).  Pointer kinds follow opts->flags
+ * of mismatches; the min(n_bad, bad_cap) LOWEST mismatching indices are
+ * written to bad_idx in ascending order (bad_idx may be NULL when bad_cap is 0).  Pointer kinds follow opts->flags
  * (n_bad/bad_idx are always host memory).  GPU only. */
 int bmqcrc_crc32c_verify(const void* arena, uint64_t arena_bytes, const uint64_t* offsets,
                          const uint32_t* lengths, const uint32_t* expected, uint64_t n,

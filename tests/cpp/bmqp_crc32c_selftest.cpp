@@ -5,6 +5,7 @@
 //
 //   bmqp_selftest            CPU cases 1-5, 7, 8 (+ fuzz property)
 //   bmqp_selftest gpu        additionally calculateBatch on the MI355X
+#include "bmqcrc_protocol.h"
 #include "bmqp_crc32c.h"
 
 #include <stdio.h>
@@ -216,6 +217,125 @@ static void fuzz_blob_equals_raw()
     }
 }
 
+// ---- protocol walks (include/bmqcrc_protocol.h) --------------------------
+static void put_be32(std::string* s, size_t at, unsigned v)
+{
+    (*s)[at] = (char)(v >> 24);
+    (*s)[at + 1] = (char)(v >> 16);
+    (*s)[at + 2] = (char)(v >> 8);
+    (*s)[at + 3] = (char)v;
+}
+
+static unsigned get_be32(const std::string& s, size_t at)
+{
+    const unsigned char* p = (const unsigned char*)s.data() + at;
+    return ((unsigned)p[0] << 24) | ((unsigned)p[1] << 16) | ((unsigned)p[2] << 8) | p[3];
+}
+
+// PUT event: EventHeader + (PutHeader(36) + app data + 1..4 padding) each,
+// CRC fields left zero (the deferred-CRC builder state).
+static std::string put_event(const std::vector<std::string>& apps)
+{
+    std::string ev(8, '\0');
+    for (const std::string& a : apps) {
+        const int pad = 4 - (int)(a.size() % 4);
+        const unsigned words = (unsigned)((36 + a.size() + pad) / 4);
+        std::string h(36, '\0');
+        put_be32(&h, 0, words);
+        put_be32(&h, 4, 9);  // headerWords
+        ev += h + a + std::string(pad, (char)pad);
+    }
+    put_be32(&ev, 0, (unsigned)ev.size());
+    ev[4] = (char)((1 << 6) | 2);  // PV 1, e_PUT
+    ev[5] = 2;
+    return ev;
+}
+
+// Cluster state ledger: file header + records (header 32 + advisory + word
+// padding + BE CRC), appendRecord's layout.
+static std::string csl_record(const std::string& adv, int type)
+{
+    std::string r(32, '\0');
+    r += adv;
+    const int pad = 4 - (int)(r.size() % 4);
+    r += std::string(pad, (char)pad);
+    r[0] = (char)((8 << 4) | type);
+    put_be32(&r, 4, (unsigned)((r.size() + 4) / 4 - 8));
+    const unsigned crc = Crc32c::calculate(r.data(), (unsigned)r.size());
+    r += std::string(4, '\0');
+    put_be32(&r, r.size() - 4, crc);
+    return r;
+}
+
+static void protocol_scans(std::vector<std::string>* apps, std::string* ev, std::string* log)
+{
+    std::mt19937 rng(21);
+    for (int i = 0; i < 300; ++i) {
+        apps->emplace_back(rng() % 3000, '\0');
+        for (auto& ch : apps->back()) {
+            ch = (char)rng();
+        }
+    }
+    *ev = put_event(*apps);
+    std::vector<unsigned long long> off(apps->size()), pos(apps->size());
+    std::vector<unsigned> len(apps->size());
+    CHECK_EQ(bmqcrc_put_event_scan(ev->data(), ev->size(), 0, 0, 0, 0), apps->size());
+    CHECK_EQ(bmqcrc_put_event_scan(ev->data(), ev->size(), (uint64_t*)off.data(), len.data(),
+                                   (uint64_t*)pos.data(), off.size()),
+             apps->size());
+    for (size_t i = 0; i < apps->size(); ++i) {
+        CHECK_EQ(len[i], (*apps)[i].size());
+        CHECK_EQ(memcmp(ev->data() + off[i], (*apps)[i].data(), len[i]), 0);
+        CHECK_EQ(pos[i] + 8, off[i]);  // CRC field at PutHeader+28, app data at +36
+    }
+    std::string bad = *ev;
+    bad[4] = 3;  // not a PUT event
+    CHECK_EQ(bmqcrc_put_event_scan(bad.data(), bad.size(), 0, 0, 0, 0), BMQCRC_EINVAL);
+
+    const unsigned char key[5] = {1, 2, 3, 4, 5};
+    *log = std::string(1, (char)((1 << 6) | 2)) + std::string((const char*)key, 5) +
+           std::string(2, '\0');
+    for (int i = 0; i < 40; ++i) {
+        *log += csl_record(std::string(1 + rng() % 500, (char)('a' + i % 26)), 1 + i % 4);
+    }
+    int walk_rc = 1;
+    uint64_t end = 0;
+    CHECK_EQ(bmqcrc_csl_scan(log->data(), log->size(), key, 0, 0, 0, 0, &walk_rc, &end), 40);
+    CHECK_EQ(walk_rc, 0);
+    CHECK_EQ(end, log->size());
+}
+
+static void gpu_protocol(const std::vector<std::string>& apps, std::string ev, std::string log)
+{
+    using namespace BloombergLP;
+    CHECK_EQ(bmqp::PutEventCrc32c::fillAll(&ev[0], ev.size()), apps.size());
+    std::vector<unsigned long long> off(apps.size());
+    std::vector<unsigned> len(apps.size());
+    bmqcrc_put_event_scan(ev.data(), ev.size(), (uint64_t*)off.data(), len.data(), 0,
+                          off.size());
+    for (size_t i = 0; i < apps.size(); ++i) {
+        CHECK_EQ(get_be32(ev, off[i] - 8), Crc32c::calculate(apps[i].data(),
+                                                             (unsigned)apps[i].size()));
+    }
+    uint64_t n = 0, nbad = 0, idx[4] = {0, 0, 0, 0};
+    CHECK_EQ(bmqp::PutEventCrc32c::verifyAll(ev.data(), ev.size(), &n, &nbad, idx, 4), 0);
+    CHECK_EQ(nbad, 0u);
+    ev[off[7]] ^= 1;
+    CHECK_EQ(bmqp::PutEventCrc32c::verifyAll(ev.data(), ev.size(), &n, &nbad, idx, 4), 0);
+    CHECK_EQ(n, apps.size());
+    CHECK_EQ(nbad, 1u);
+    CHECK_EQ(idx[0], 7u);
+
+    const unsigned char key[5] = {1, 2, 3, 4, 5};
+    uint64_t offset = 0;
+    CHECK_EQ(mqbc::ClusterStateLedgerCrc32c::validateLog(&offset, log.data(), log.size(), key),
+             0);
+    CHECK_EQ(offset, log.size());
+    log[8 + 32] ^= 1;  // first advisory byte of the first record
+    CHECK_EQ(mqbc::ClusterStateLedgerCrc32c::validateLog(&offset, log.data(), log.size(), key),
+             BMQCRC_CSL_INVALID_CHECKSUM);
+}
+
 static void gpu_batch()
 {
     if (bmqcrc_device_count() <= 0) {
@@ -279,8 +399,12 @@ int main(int argc, char** argv)
     test5_multithreaded();
     test7_8_blob();
     fuzz_blob_equals_raw();
+    std::vector<std::string> apps;
+    std::string ev, log;
+    protocol_scans(&apps, &ev, &log);
     if (argc > 1 && strcmp(argv[1], "gpu") == 0) {
         gpu_batch();
+        gpu_protocol(apps, ev, log);
     } else {
         // without a GPU the batch path must refuse loudly, never fall back
         unsigned out = 0;

@@ -1,5 +1,6 @@
-"""The C-ABI library loads and exports every entry point include/bmqcrc.h
-declares (no compute on a GPU here)."""
+"""The C-ABI library loads and exports every entry point include/bmqcrc.h and
+include/bmqcrc_protocol.h declare, and nothing else under the bmqcrc_ prefix
+(no compute on a GPU here)."""
 import ctypes
 import os
 import re
@@ -9,9 +10,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "blazingmq_amd", "lib", "libbmqcrc.so")
 
 
+HEADERS = ("bmqcrc.h", "bmqcrc_protocol.h")
+
+
 def declared():
-    with open(os.path.join(ROOT, "include", "bmqcrc.h")) as f:
-        src = f.read()
+    src = ""
+    for h in HEADERS:
+        with open(os.path.join(ROOT, "include", h)) as f:
+            src += f.read()
     return sorted(set(re.findall(r"^\w[\w\s\*]*?\b(bmqcrc_\w+)\s*\(", src, re.M)))
 
 
@@ -20,7 +26,10 @@ def test_header_declares_expected_api():
     for n in ("bmqcrc_crc32c", "bmqcrc_crc32c_blob", "bmqcrc_combine", "bmqcrc_crc32c_batch",
               "bmqcrc_crc32c_batch_multi", "bmqcrc_reserve", "bmqcrc_fill_synthetic",
               "bmqcrc_kernel_timing", "bmqcrc_device_count", "bmqcrc_last_error",
-              "bmqcrc_version"):
+              "bmqcrc_version", "bmqcrc_crc32c_verify", "bmqcrc_crc32c_blobs",
+              "bmqcrc_put_event_scan", "bmqcrc_put_event_fill_crcs", "bmqcrc_put_event_verify",
+              "bmqcrc_journal_scan", "bmqcrc_recover_verify", "bmqcrc_csl_scan",
+              "bmqcrc_csl_validate"):
         assert n in names
 
 
@@ -31,6 +40,8 @@ def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True).stdout
     exported = set(l.split()[-1] for l in out.splitlines() if l.strip())
     assert set(declared()) <= exported
+    # internal launchers and error hooks stay hidden
+    assert set(n for n in exported if n.startswith("bmqcrc_")) == set(declared())
 
 
 def test_library_contains_gfx950_code_object():

@@ -1,13 +1,15 @@
 """GPU parts of SURVEY 8(f): batched recovery verification, deferred-CRC PUT
-events and the batched Blob overload -- all through the C ABI, bit-exact
-against the oracle and the reference's fixtures."""
+events and their batched iterator check, the batched Blob overload, and the
+cluster state ledger's validateLog -- all through the C ABI
+(include/bmqcrc.h, include/bmqcrc_protocol.h), bit-exact against the oracle
+and the reference's fixtures."""
 import os
 
 import numpy as np
 import pytest
 
 import oracle
-from blazingmq_amd import Blob, Crc32c, storage
+from blazingmq_amd import Blob, Crc32c, csl, storage
 from blazingmq_amd.put_event import PutEventBuilder, PutMessageIterator
 
 pytestmark = pytest.mark.gpu
@@ -28,17 +30,23 @@ def test_verify_detects_exact_corruptions(cuda):
     j, d = storage.write_partition(apps)
     res = storage.verify_partition(j, d)
     assert res["n_bad"] == 0 and res["n_messages"] == len(apps)
+    scan = storage.scan_partition(j, d)
     # flip one byte in the payload of some messages, and one stored CRC
     victims = sorted(set(int(i) for i in rng.integers(0, len(apps), size=37)
                          if sizes[int(i)] > 0))
     for i in victims:
-        o = int(res["app_offset"][i]) + int(rng.integers(0, sizes[i]))
+        o = int(scan["app_offset"][i]) + int(rng.integers(0, sizes[i]))
         d[o] ^= 0x01
     jcrc_victim = next(i for i in range(len(apps)) if i not in victims)
-    rec = int(res["records"]["record_offset"][jcrc_victim])
+    rec = int(scan["record_offset"][jcrc_victim])
     j[rec + 55] ^= 0x80
     res2 = storage.verify_partition(j, d)
-    assert res2["bad_index"].tolist() == sorted(victims + [jcrc_victim])
+    want = scan["record_offset"][sorted(victims + [jcrc_victim])]
+    assert res2["n_bad"] == len(want)
+    assert res2["bad_record_offsets"].tolist() == want.tolist()
+    # bounded report: the first bad_cap offsets, full count
+    res3 = storage.verify_partition(j, d, bad_cap=5)
+    assert res3["n_bad"] == len(want) and res3["bad_record_offsets"].tolist() == want[:5].tolist()
 
 
 def test_put_event_deferred_equals_immediate(cuda):
@@ -53,6 +61,56 @@ def test_put_event_deferred_equals_immediate(cuda):
         evs.append(b.finalize())
     assert np.array_equal(evs[0], evs[1])
     assert [m["crc32c"] for m in PutMessageIterator(evs[1])] == [oracle.crc32c(a) for a in apps]
+    # the iterator-side batched check (bmqp_putmessageiterator.cpp:670-679)
+    it = PutMessageIterator(evs[1])
+    n, n_bad, bad = it.verify_crcs()
+    assert (n, n_bad, bad.size) == (len(apps), 0, 0)
+    off, ln, _ = it.scan()
+    victims = [i for i in (3, 77, 499) if ln[i] > 0]
+    ev = evs[1].copy()
+    for i in victims:
+        ev[int(off[i]) + int(ln[i]) // 2] ^= 0x10
+    n, n_bad, bad = PutMessageIterator(ev).verify_crcs()
+    assert (n, n_bad, bad.tolist()) == (len(apps), len(victims), victims)
+
+
+def _csl_log(n, rng, key=b"\x01\x02\x03\x04\x05"):
+    recs = [csl.append_record(rng.integers(0, 256, size=int(rng.integers(1, 3000)),
+                                           dtype=np.uint8).tobytes(),
+                              record_type=int(rng.integers(1, 5)), elector_term=3,
+                              sequence_number=i + 1, timestamp=123567 + i)
+            for i in range(n)]
+    return csl.file_header(key) + b"".join(recs), recs
+
+
+def test_csl_validate_log(cuda):
+    rng = np.random.default_rng(12)
+    key = b"\x01\x02\x03\x04\x05"
+    log, recs = _csl_log(3, rng, key)
+    # mqbc_clusterstateledgerutil.t.cpp test4: valid log, then a record whose
+    # size runs past the end of the log
+    assert csl.validate_log(log, key) == (csl.SUCCESS, len(log), None)
+    bad_hdr = bytes(csl.record_header(csl.UPDATE, 400))
+    rc, _, _ = csl.validate_log(log + bad_hdr, key)
+    assert rc == csl.REACHED_END_OF_LOG
+    # test5: a record with an incorrect CRC
+    wrong = csl.append_record(b"advisory", csl.UPDATE, 3, 8, 123567, crc=111111)
+    assert csl.validate_log(log + wrong, key) == (csl.INVALID_CHECKSUM, 0, len(log))
+    # a cleanly invalid record header ends the walk with success
+    zeros = bytes(64)
+    assert csl.validate_log(log + zeros, key) == (csl.SUCCESS, len(log), None)
+    assert csl.validate_log(log, b"\x09" * 5)[0] == csl.INVALID_LOG_ID
+
+
+def test_csl_validate_large_log_first_bad(cuda):
+    rng = np.random.default_rng(13)
+    log, recs = _csl_log(5000, rng)
+    ends = np.cumsum([csl.FILE_HEADER_SIZE] + [len(r) for r in recs])
+    assert csl.validate_log(log)[:2] == (csl.SUCCESS, len(log))
+    b = bytearray(log)
+    for k in (4100, 1234, 2500):  # the earliest corrupt record is reported
+        b[int(ends[k]) + csl.RECORD_HEADER_SIZE] ^= 0x01  # first advisory byte
+    assert csl.validate_log(bytes(b)) == (csl.INVALID_CHECKSUM, 0, int(ends[1234]))
 
 
 def test_blobs_batch(cuda, golden):

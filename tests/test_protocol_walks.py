@@ -1,0 +1,203 @@
+"""Native protocol walks (include/bmqcrc_protocol.h) on the CPU: the PUT
+event, partition (journal + DATA) and cluster-state-ledger scans agree with
+the numpy restatements and the reference's fixture, reject malformed input
+the way the reference does, and the GPU-only entry points refuse loudly
+without a device (no CPU fallback)."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from blazingmq_amd import _native as N
+from blazingmq_amd import csl, storage
+from blazingmq_amd.put_event import PutEventBuilder, PutMessageIterator
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+NO_GPU = N.lib.bmqcrc_device_count() == 0
+
+
+def _event(apps, options=b""):
+    b = PutEventBuilder(defer_crc=False)
+    for i, a in enumerate(apps):
+        b.pack_message(a, queue_id=i, options=options if i % 3 == 0 else b"")
+    return b.finalize()
+
+
+def test_put_scan_matches_iterator():
+    rng = np.random.default_rng(1)
+    apps = [rng.integers(0, 256, size=int(n), dtype=np.uint8).tobytes()
+            for n in list(range(9)) + list(rng.integers(0, 5000, size=200))]
+    ev = _event(apps, options=b"\x00" * 8)
+    it = PutMessageIterator(ev)
+    off, ln, pos = it.scan()
+    msgs = list(it)
+    assert off.tolist() == [m["app_offset"] for m in msgs]
+    assert ln.tolist() == [len(a) for a in apps]
+    for p, m, a in zip(pos, msgs, apps):
+        assert int.from_bytes(ev[int(p):int(p) + 4].tobytes(), "big") == m["crc32c"]
+        assert m["crc32c"] == oracle.crc32c(a)
+    empty = PutEventBuilder(defer_crc=False).finalize()
+    assert [x.size for x in PutMessageIterator(empty).scan()] == [0, 0, 0]
+
+
+@pytest.mark.parametrize("mutate", ["length", "type", "truncated", "pad0", "pad5", "words"])
+def test_put_scan_rejects_malformed(mutate):
+    ev = _event([b"abcdef", b"x" * 100]).copy()
+    first = 8
+    if mutate == "length":
+        ev[3] ^= 4
+    elif mutate == "type":
+        ev[4] = (ev[4] & 0xC0) | 3
+    elif mutate == "truncated":
+        ev = ev[:-3].copy()
+        ev[0:4] = np.frombuffer(ev.size.to_bytes(4, "big"), np.uint8)
+    elif mutate == "pad0":
+        msg = (int.from_bytes(ev[first:first + 4].tobytes(), "big") & 0x0FFFFFFF) * 4
+        ev[first + msg - 1] = 0
+    elif mutate == "pad5":
+        msg = (int.from_bytes(ev[first:first + 4].tobytes(), "big") & 0x0FFFFFFF) * 4
+        ev[first + msg - 1] = 5
+    elif mutate == "words":
+        ev[first + 3] = 0xFF  # messageWords beyond the event
+    it = PutMessageIterator.__new__(PutMessageIterator)  # skip the Python-side checks
+    it.ev = ev
+    with pytest.raises(N.BmqCrcError) as e:
+        it.scan()
+    assert e.value.rc == N.BMQCRC_EINVAL
+
+
+def _fixture():
+    return (np.fromfile(os.path.join(GOLD, "test.bmq_journal"), np.uint8),
+            np.fromfile(os.path.join(GOLD, "test.bmq_data"), np.uint8))
+
+
+def test_partition_scan_fixture(golden):
+    j, d = _fixture()
+    s = storage.scan_partition(j, d)
+    assert s["record_offset"].tolist() == golden["journal_file"]["message_record_offsets"]
+    assert s["crc32c"].tolist() == golden["journal_file"]["crc"]
+    assert s["app_offset"].tolist() == [52, 76] and s["app_length"].tolist() == [11, 11]
+
+
+def test_partition_scan_matches_numpy_walk():
+    rng = np.random.default_rng(2)
+    sizes = list(range(20)) + list(rng.integers(0, 40000, size=500))
+    apps = [rng.integers(0, 256, size=int(n), dtype=np.uint8).tobytes() for n in sizes]
+    j, d = storage.write_partition(apps)
+    s = storage.scan_partition(j, d)
+    r = storage.journal_message_records(j)
+    off, ln = storage.data_app_ranges(d, r["data_offset"])
+    assert s["record_offset"].tolist() == r["record_offset"].tolist()
+    assert s["app_offset"].tolist() == off.tolist() and s["app_length"].tolist() == ln.tolist()
+    assert s["crc32c"].tolist() == r["crc32c"].tolist() == [oracle.crc32c(a) for a in apps]
+    # zero-filled (pre-allocated) journal tail ends the walk
+    jz = np.concatenate([j, np.zeros(60 * 7, np.uint8)])
+    assert storage.scan_partition(jz, d)["record_offset"].size == len(apps)
+
+
+@pytest.mark.parametrize("mutate", ["jmagic", "dmagic", "rec_magic", "beyond", "padding",
+                                    "zero_words"])
+def test_partition_scan_rejects_malformed(mutate):
+    j, d = storage.write_partition([b"hello world", b"x" * 77])
+    j, d = j.copy(), d.copy()
+    rec0 = storage.scan_partition(j, d)["record_offset"][0]
+    if mutate == "jmagic":
+        j[0] ^= 1
+    elif mutate == "dmagic":
+        d[4] ^= 1
+    elif mutate == "rec_magic":
+        j[int(rec0) + 57] ^= 1
+    elif mutate == "beyond":
+        j[int(rec0) + 32:int(rec0) + 36] = np.frombuffer((10**6).to_bytes(4, "big"), np.uint8)
+    elif mutate == "padding":
+        d[40 + 12 + 11] = 9   # "hello world" record: 12 B header + 11 B + 1 pad byte
+    elif mutate == "zero_words":
+        d[40:44] = 0
+    with pytest.raises(storage.StorageFormatError):
+        storage.scan_partition(j, d)
+
+
+KEY = b"\x11\x22\x33\x44\x55"
+
+
+def _log(n, seed=3):
+    rng = np.random.default_rng(seed)
+    recs = [csl.append_record(rng.integers(0, 256, size=int(rng.integers(1, 700)),
+                                           dtype=np.uint8).tobytes(),
+                              record_type=1 + i % 4, elector_term=3, sequence_number=i + 1,
+                              timestamp=123567)
+            for i in range(n)]
+    return csl.file_header(KEY) + b"".join(recs), recs
+
+
+def test_csl_record_layout():
+    adv = b"advisory!"  # 32 + 9 = 41 bytes -> 11 words, 3 padding bytes
+    r = csl.append_record(adv, csl.COMMIT, elector_term=3, sequence_number=9, timestamp=123678)
+    assert len(r) == 32 + 9 + 3 + 4
+    assert r[0] == (8 << 4) | csl.COMMIT
+    assert int.from_bytes(r[4:8], "big") == (len(r) - 32) // 4  # LeaderAdvisoryWords
+    assert r[41:44] == b"\x03\x03\x03"
+    assert int.from_bytes(r[-4:], "big") == oracle.crc32c(r[:-4])
+    assert csl.file_header(KEY) == bytes([0x42]) + KEY + b"\x00\x00"
+
+
+def test_csl_scan_walk():
+    log, recs = _log(50)
+    wrc, end, off, ln, crc = csl.scan_log(log, KEY)
+    assert (wrc, end) == (0, len(log))
+    starts = np.cumsum([8] + [len(r) for r in recs])[:-1]
+    assert off.tolist() == starts.tolist()
+    assert ln.tolist() == [len(r) - 4 for r in recs]
+    assert crc.tolist() == [oracle.crc32c(r[:-4]) for r in recs]
+    # an invalid record header (undefined type) stops the walk cleanly
+    stop = bytearray(csl.record_header(0, 5)) + bytes(20)
+    assert csl.scan_log(log + bytes(stop), KEY)[:2] == (0, len(log))
+    # a trailing partial header is not walked
+    assert csl.scan_log(log + bytes(31), KEY)[:2] == (0, len(log))
+    # a record running past the end (reference test4) -> e_REACHED_END_OF_LOG
+    assert csl.scan_log(log + bytes(csl.record_header(csl.UPDATE, 400)))[0] == \
+        csl.REACHED_END_OF_LOG
+
+
+@pytest.mark.parametrize("case,rc", [("pv", csl.INVALID_PROTOCOL_VERSION),
+                                     ("nullkey", csl.INVALID_LOG_ID),
+                                     ("wrongkey", csl.INVALID_LOG_ID),
+                                     ("hw0", csl.INVALID_HEADER_WORDS),
+                                     ("short", csl.REACHED_END_OF_LOG * 100 +
+                                      csl.RECORD_ALIAS_FAILURE)])
+def test_csl_file_header_codes(case, rc):
+    log, _ = _log(2)
+    b = bytearray(log)
+    key = KEY
+    if case == "pv":
+        b[0] = (2 << 6) | 2
+    elif case == "nullkey":
+        b[1:6] = bytes(5)
+    elif case == "wrongkey":
+        key = b"\x00\x00\x00\x00\x01"
+    elif case == "hw0":
+        b[0] = 1 << 6
+    elif case == "short":
+        b = b[:7]
+    assert csl.scan_log(bytes(b), key)[0] == rc
+
+
+@pytest.mark.skipif(not NO_GPU, reason="checks the no-device refusal")
+def test_gpu_only_walks_refuse_without_device():
+    j, d = _fixture()
+    with pytest.raises(N.BmqCrcError) as e:
+        storage.verify_partition(j, d)
+    assert e.value.rc == N.BMQCRC_ENODEV
+    b = PutEventBuilder(defer_crc=True)
+    b.pack_message(b"payload")
+    with pytest.raises(N.BmqCrcError) as e:
+        b.finalize()
+    assert e.value.rc == N.BMQCRC_ENODEV
+    with pytest.raises(N.BmqCrcError) as e:
+        PutMessageIterator(_event([b"abc"])).verify_crcs()
+    assert e.value.rc == N.BMQCRC_ENODEV
+    log, _ = _log(2)
+    with pytest.raises(N.BmqCrcError) as e:
+        csl.validate_log(log, KEY)
+    assert e.value.rc == N.BMQCRC_ENODEV
