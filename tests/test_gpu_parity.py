@@ -113,6 +113,30 @@ def test_random_vs_oracle(cuda, seg_bytes):
     assert bad.size == 0, [(int(i), int(offs[i]), int(lens[i])) for i in bad[:10]]
 
 
+def test_small_ragged_batches(cuda):
+    # Small mixed batches (a PUT event's worth of messages): the planner's
+    # size-class sort puts a message's segments into different buckets, so a
+    # wave can hold one message in two separate lane runs.
+    import torch
+    rng = np.random.default_rng(4321)
+    arena_np = rng.integers(0, 256, size=4 << 20, dtype=np.uint8)
+    arena = torch.from_numpy(arena_np).to(cuda)
+    for t in range(240):
+        n = int(rng.integers(2, 70))
+        seg = int(rng.choice([0, 0, 256, 384, 512, 1024]))
+        hi = 100000 if seg == 0 else 3000
+        lens = rng.integers(0, hi, size=n).astype(np.uint32)
+        offs = np.array([rng.integers(0, arena_np.size - l + 1) for l in lens], np.int64)
+        seeds = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+        got = Crc32c.calculate_batch(arena, torch.from_numpy(offs).to(cuda),
+                                     torch.from_numpy(lens.astype(np.int32)).to(cuda),
+                                     torch.from_numpy(seeds.view(np.int32)).to(cuda),
+                                     seg_bytes=seg).cpu().numpy().view(np.uint32)
+        exp = oracle.batch(arena_np, offs, lens, seeds)
+        bad = np.nonzero(got != exp)[0]
+        assert bad.size == 0, (t, seg, [(int(i), int(offs[i]), int(lens[i])) for i in bad[:5]])
+
+
 def test_line_boundary_edges(cuda):
     # starts near the end of a 128-byte line (seed word crossing lines), tiny lengths
     rng = np.random.default_rng(7)
