@@ -433,244 +433,6 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
 
     const uint32_t stride = gridDim.x * kWavesPerBlock;
     const uint32_t seg_shift = (SEG & (SEG - 1u)) == 0 ? (uint32_t)__builtin_ctz(SEG) : 0u;
-    uint32_t g = blockIdx.x * kWavesPerBlock + wave;
-    if (g >= ngroups) {
-        return;  // no barrier follows
-    }
-    auto seg_valid = [&](uint32_t grp) {
-        return grp < ngroups && grp * 64u + (uint32_t)lane < total;
-    };
-    auto seg_map = [&](uint32_t grp) {
-        return map_segment(a, grp * 64u + (uint32_t)lane, seg_valid(grp), identity, uni, sorted);
-    };
-    auto nsegs = [&](uint32_t len) {
-        return (seg_shift ? ((len - 1u) >> seg_shift) : (len - 1u) / SEG) + 1u;
-    };
-
-    // Software pipeline over the wave's groups.  Rounds of consecutive groups
-    // form one stream: round t uses LDS slot t & 1 and round t + 2 is issued
-    // as soon as round t has been read, even when it belongs to the next
-    // group, so the next group's first lines are in flight while this group
-    // finishes (tail, move, combine).  Descriptors run two groups ahead and
-    // the segment map three; their loads are issued just before the next
-    // group's first DMA round.  The prefetch point starts with vmcnt(0): it
-    // lands this group's remaining rounds (the compiler would wait there for
-    // the descriptors anyway), so rounds read after it need no wait and the
-    // fresh descriptor loads never stall a round.
-    //
-    // DMA addresses of the group whose rounds are being issued: lane l of
-    // instruction i serves segment 8i + l/8, piece p of its line.
-    uint64_t dbase[8];
-    uint32_t dlim[8];  // lines of data of that segment (0: none)
-    uint64_t dummy;
-    uint32_t rounds_next = 0;  // R of the group whose DMA is set up
-    auto dma_setup = [&](const SegDesc& d, bool v) {
-        const uint32_t len = d.len;
-        const uint32_t ns = v ? nsegs(len) : 0u;
-        const SegGeom gg = seg_geom(arena + d.off, len, d.k, ns, SEG);
-        const uint64_t l0 = gg.L0;
-        const uint32_t nld = v ? gg.nl_data : 0u;
-        rounds_next = wave_max(v ? gg.nl : 0u);
-        // lane 0 always holds a valid segment; its first line is the dummy
-        dummy = rfl64(l0) + 16u * ((uint32_t)lane & 7u);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int src = 8 * i + (lane >> 3);
-            const uint32_t p = ((uint32_t)lane & 7u) ^ ((4u * i + ((uint32_t)lane >> 4)) & 7u);
-            dbase[i] = shfl64(l0, src) + 16u * p;
-            dlim[i] = (uint32_t)__shfl((int)nld, src);
-        }
-    };
-
-    // prologue: descriptors of this group and the next, map of the one after
-    SegDesc cur = fetch_desc(a, seg_map(g), seg_valid(g));
-    SegDesc nxt = fetch_desc(a, seg_map(g + stride), seg_valid(g + stride));
-    SegRef ref2 = seg_map(g + 2u * stride);
-    dma_setup(cur, seg_valid(g));
-    uint32_t R = rounds_next;
-    dma_round<NT>(wave_lds, dbase, dlim, dummy, 0);
-    if (R > 1) {
-        dma_round<NT>(wave_lds + kSlotBytes, dbase, dlim, dummy, 1);
-    }
-    uint32_t par = 0;  // slot of this group's round 0
-
-    for (;;) {
-        const uint32_t seg = g * 64u + (uint32_t)lane;
-        const bool valid = seg < total;
-        const bool has_next = g + stride < ngroups;
-        const uint32_t msg = cur.msg, k = cur.k, len = cur.len, seed = cur.seed;
-        const uint32_t nseg = valid ? nsegs(len) : 0u;
-        const uint64_t mstart = arena + cur.off;
-        const uint64_t mend = mstart + len;
-        const SegGeom geo = seg_geom(mstart, len, k, nseg, SEG);
-        const uint64_t S = geo.S, E = geo.E, L0 = geo.L0;
-        const bool first = valid && k == 0;
-        const uint32_t nl = valid ? geo.nl : 0u;
-
-        // Set up the next group's DMA and issue its round 0 into `slot`, after
-        // issuing the descriptor loads two and three groups ahead.
-        SegDesc nxt2;
-        SegRef ref3;
-        auto prefetch = [&](uint32_t slot) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            dma_setup(nxt, seg_valid(g + stride));
-            nxt2 = fetch_desc(a, ref2, seg_valid(g + 2u * stride));
-            ref3 = seg_map(g + 3u * stride);
-            dma_round<NT>(slot, dbase, dlim, dummy, 0);
-        };
-        uint32_t rn = 0;  // next group's R (0: not set up)
-        if (R == 1 && has_next) {
-            prefetch(wave_lds + ((par + 1u) & 1u) * kSlotBytes);
-            rn = rounds_next;
-        }
-
-        // ------------------------------------------------------ fold rounds
-        uint32_t q[32];
-#pragma unroll
-        for (int d = 0; d < 32; ++d) {
-            q[d] = 0;
-        }
-        uint32_t crc = 0;
-        const uint32_t c0 = ~seed;
-        const uint64_t inj_end = first ? S + 4 : S;
-
-        for (uint32_t r = 0; r < R; ++r) {
-            const uint32_t slot = wave_lds + ((par + r) & 1u) * kSlotBytes;
-            if (rn == 0) {  // no prefetch yet in this group (it waits vmcnt(0) itself)
-                if (r + 1 < R) {
-                    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // round r + 1 stays in flight
-                } else {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                }
-            }
-            uint32_t m[32];
-#pragma unroll
-            for (int kk = 0; kk < 8; ++kk) {
-                const u32x4 v = *(lds_cu4*)(uintptr_t)(slot + (rd_off ^ (16u * kk)));
-                m[4 * kk + 0] = v.x;
-                m[4 * kk + 1] = v.y;
-                m[4 * kk + 2] = v.z;
-                m[4 * kk + 3] = v.w;
-            }
-            if (r + 2 < R) {
-                dma_round<NT>(slot, dbase, dlim, dummy, r + 2);
-            } else if (r + 2 == R && has_next) {
-                prefetch(slot);  // next group's round 0
-                rn = rounds_next;
-            } else if (r + 1 == R && has_next && rn > 1) {
-                dma_round<NT>(slot, dbase, dlim, dummy, 1);  // next group's round 1
-            }
-            // Zero the bytes outside [S, E) and XOR the seed word in at S; each
-            // step runs only when some lane of the wave needs it this round.
-            const uint64_t p0 = L0 + ((uint64_t)r << 7);
-            const bool live = r < nl;
-            const bool lo_cut = live && p0 < S;           // first line, unaligned start
-            const bool hi_cut = live && p0 + 128u > E;    // last line(s): bytes from E on
-            const bool inj = live && p0 < inj_end && S < p0 + 128u;  // seed word here
-            if (__ballot(lo_cut)) {
-                mask_lo(m, lo_cut ? (int)(S - p0) : 0);
-            }
-            if (__ballot(hi_cut)) {
-                mask_hi(m, hi_cut ? (int)(E > p0 ? E - p0 : 0) : 128);
-            }
-            if (__ballot(inj && S != p0)) {
-                inject_seed(m, inj ? (int)((int64_t)S - (int64_t)p0) : -64, c0);
-            } else if (inj) {
-                m[0] ^= c0;  // line-aligned message start: the seed is word 0
-            }
-            if (r + 1 < nl) {
-                fold_round(q, m);
-            } else if (r + 1 == nl) {
-                crc = tail_round(q, m, tab_lds);
-            }
-        }
-
-        // ------------------------------------------------ move + combine
-        // raw(stream) = raw(segment) * x^(8 padE): un-shift the zero padding
-        // (table x^-8p + one 160-VALU multiply), then move the segment to the
-        // message end with x^(8 after) (sparse exponent: bits no lane needs are
-        // skipped wave-uniformly).
-        uint32_t contrib = 0;
-        const uint32_t padE = valid ? (uint32_t)(L0 + ((uint64_t)nl << 7) - E) : 0u;
-        if (__ballot(padE != 0) == 0) {
-            contrib = valid ? crc : 0u;
-        } else if (valid) {
-            contrib = gmul(crc, c_xneg8[padE]);
-        }
-        const uint32_t e_after = valid ? mersenne31(8ull * (mend - E)) : 0u;
-        contrib = mul_xpow(contrib, e_after);
-        if (first) {
-            contrib ^= 0xffffffffu;
-        }
-        // XOR-reduce each run of adjacent lanes holding the same message, then
-        // one store or atomic per run: the run head owns the result.  A
-        // message may occupy several runs of one wave (the size-class sort
-        // can split its segments across a bucket boundary inside the wave),
-        // so runs are delimited by a head ballot, never by key equality, and
-        // a head stores plainly only when its run is the whole message.
-        const uint32_t key = valid ? msg : 0xffffffffu;
-        const uint32_t pkey = (uint32_t)__shfl_up((int)key, 1);
-        const bool head = lane == 0 || pkey != key;
-        const uint64_t heads = __ballot(head);
-        const uint64_t upto = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
-        const uint64_t later = heads & ~upto;
-        const uint32_t rend = later ? (uint32_t)__builtin_ctzll(later) : 64u;  // run end
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t ov = (uint32_t)__shfl_down((int)contrib, o);
-            if ((uint32_t)lane + (uint32_t)o < rend) {
-                contrib ^= ov;
-            }
-        }
-        if (valid && head) {
-            if (k == 0 && rend - (uint32_t)lane == nseg) {
-                a.out[msg] = contrib;  // the whole message is this run
-            } else {
-                atomicXor(&a.out[msg], contrib);
-            }
-        }
-        if (!has_next) {
-            break;
-        }
-        par = (par + R) & 1u;
-        R = rn;
-        g += stride;
-        cur = nxt;
-        nxt = nxt2;
-        ref2 = ref3;
-    }
-}
-
-// EXPERIMENT: pre-pipeline loop (A/B via BMQCRC_TUNE bit 4)
-template <bool NT>
-__global__ __launch_bounds__(256, 2) void k_fold_v1(BatchArgs a)
-{
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kTabBytes + kLdsBytes];
-
-    const int lane = threadIdx.x & 63;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t tab_lds = (uint32_t)(uintptr_t)(lds_u8*)lds;
-    const uint32_t wave_lds = tab_lds + kTabBytes + wave * (kSlots * kSlotBytes);
-
-    // remainder-reduction tables -> LDS (8 KiB, once per block; no DMA in flight yet)
-    for (uint32_t t = threadIdx.x; t < 8u * 256u; t += blockDim.x) {
-        *(__attribute__((address_space(3))) uint32_t*)(uintptr_t)(tab_lds + 4u * t) =
-            c_ty[t >> 8][t & 255u];
-    }
-    __syncthreads();
-
-    const uint32_t total = a.ctrl->total_segs;
-    const uint32_t identity = a.ctrl->identity;
-    const uint32_t sorted = a.ctrl->sorted;
-    const uint32_t uni = a.ctrl->nseg_uniform;
-    const uint32_t ngroups = (total + 63u) / 64u;
-    const uint32_t SEG = a.seg_bytes;
-    const uint64_t arena = (uint64_t)(uintptr_t)a.arena;
-
-    const uint32_t rd_off = (uint32_t)lane * 128u + (((uint32_t)lane >> 1) & 7u) * 16u;
-
-    const uint32_t stride = gridDim.x * kWavesPerBlock;
-    const uint32_t seg_shift = (SEG & (SEG - 1u)) == 0 ? (uint32_t)__builtin_ctz(SEG) : 0u;
     // Descriptor pipeline across groups: the (message, part) of the group
     // after next and the (offset, length, seed) of the next group are loaded
     // while the current group folds, so no group starts on a cold load.
@@ -756,11 +518,13 @@ __global__ __launch_bounds__(256, 2) void k_fold_v1(BatchArgs a)
             if (r + 2 < R) {
                 dma_round<NT>(slot, dbase, dlim, dummy, r + 2);
             }
+            // Zero the bytes outside [S, E) and XOR the seed word in at S; each
+            // step runs only when some lane of the wave needs it this round.
             const uint64_t p0 = L0 + ((uint64_t)r << 7);
             const bool live = r < nl;
-            const bool lo_cut = live && p0 < S;
-            const bool hi_cut = live && p0 + 128u > E;
-            const bool inj = live && p0 < inj_end && S < p0 + 128u;
+            const bool lo_cut = live && p0 < S;           // first line, unaligned start
+            const bool hi_cut = live && p0 + 128u > E;    // last line(s): bytes from E on
+            const bool inj = live && p0 < inj_end && S < p0 + 128u;  // seed word here
             if (__ballot(lo_cut)) {
                 mask_lo(m, lo_cut ? (int)(S - p0) : 0);
             }
@@ -770,7 +534,7 @@ __global__ __launch_bounds__(256, 2) void k_fold_v1(BatchArgs a)
             if (__ballot(inj && S != p0)) {
                 inject_seed(m, inj ? (int)((int64_t)S - (int64_t)p0) : -64, c0);
             } else if (inj) {
-                m[0] ^= c0;
+                m[0] ^= c0;  // line-aligned message start: the seed is word 0
             }
             if (r + 1 < nl) {
                 fold_round(q, m);
@@ -799,13 +563,19 @@ __global__ __launch_bounds__(256, 2) void k_fold_v1(BatchArgs a)
         // XOR-reduce the runs of lanes that hold segments of the same message
         // (segments of a message are consecutive), then one store or atomic
         // per run: the run head owns the result.
+        // XOR-reduce each run of adjacent lanes holding the same message, then
+        // one store or atomic per run: the run head owns the result.  A
+        // message may occupy several runs of one wave (the size-class sort
+        // can split its segments across a bucket boundary inside the wave),
+        // so runs are delimited by a head ballot, never by key equality, and
+        // a head stores plainly only when its run is the whole message.
         const uint32_t key = valid ? msg : 0xffffffffu;
         const uint32_t pkey = (uint32_t)__shfl_up((int)key, 1);
         const bool head = lane == 0 || pkey != key;
         const uint64_t heads = __ballot(head);
         const uint64_t upto = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
         const uint64_t later = heads & ~upto;
-        const uint32_t rend = later ? (uint32_t)__builtin_ctzll(later) : 64u;
+        const uint32_t rend = later ? (uint32_t)__builtin_ctzll(later) : 64u;  // run end
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t ov = (uint32_t)__shfl_down((int)contrib, o);
@@ -815,7 +585,7 @@ __global__ __launch_bounds__(256, 2) void k_fold_v1(BatchArgs a)
         }
         if (valid && head) {
             if (k == 0 && rend - (uint32_t)lane == nseg) {
-                a.out[msg] = contrib;
+                a.out[msg] = contrib;  // the whole message is this run
             } else {
                 atomicXor(&a.out[msg], contrib);
             }
@@ -1324,11 +1094,7 @@ extern "C" int bmqcrc_launch_batch(const BatchArgs* a, void* stream, int num_cus
         (void)hipEventRecord((hipEvent_t)ev_start, s);
     }
     if (!(a->tune & 1u)) {  // default: non-temporal LDS-DMA (once-read stream)
-        if (a->tune & 4u) {
-            hipLaunchKernelGGL(k_fold_v1<true>, dim3((unsigned)grid), dim3(kWavesPerBlock * 64), 0, s, *a);
-        } else {
-            hipLaunchKernelGGL(k_fold<true>, dim3((unsigned)grid), dim3(kWavesPerBlock * 64), 0, s, *a);
-        }
+        hipLaunchKernelGGL(k_fold<true>, dim3((unsigned)grid), dim3(kWavesPerBlock * 64), 0, s, *a);
     } else {
         hipLaunchKernelGGL(k_fold<false>, dim3((unsigned)grid), dim3(kWavesPerBlock * 64), 0, s,
                            *a);
