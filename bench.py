@@ -61,6 +61,8 @@ CONFIGS = {
                     _uniform(16, 256 << 20), 5, "weak"),
 }
 
+UNIFORM_SIZES = {"64k_x_64KiB": 65536, "1M_x_256B": 256, "16_x_256MiB": 256 << 20}
+
 
 def parse():
     p = argparse.ArgumentParser()
@@ -69,6 +71,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", default="64k_x_64KiB", choices=list(CONFIGS))
     p.add_argument("--seg-bytes", type=int, default=0)
+    p.add_argument("--msgs", type=int, default=0,
+                   help="experiment: override the message count of a uniform config "
+                        "(the line is then marked as not the BASELINE workload)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=2.0,
                    help="approximate wall time of the CPU-baseline sample")
@@ -160,6 +165,10 @@ def main():
     dev = torch.device("cuda", local)
 
     desc, gen, seed, scaling = CONFIGS[args.config]
+    if args.msgs:
+        size = UNIFORM_SIZES[args.config]  # KeyError: only uniform configs can be resized
+        gen = _uniform(args.msgs, size)
+        desc = "EXPERIMENT (not the BASELINE workload): %d msgs x %d B" % (args.msgs, size)
     lens_np, begin = gen(rank, world)
     n = int(lens_np.size)
     offs_np = np.zeros(n, dtype=np.int64)

@@ -66,6 +66,9 @@ def build_product(force=False):
               "-lpthread"])
         for o in objs:
             os.remove(o)
+        for leftover in os.listdir(LIB):  # hipcc offload-bundling intermediates
+            if leftover.startswith("libbmqcrc.so."):
+                os.remove(os.path.join(LIB, leftover))
     selftest = os.path.join(ROOT, "tests", "cpp", "bin", "bmqp_selftest")
     st_src = os.path.join(ROOT, "tests", "cpp", "bmqp_crc32c_selftest.cpp")
     if os.path.exists(st_src) and (force or _stale(selftest, [st_src, target])):

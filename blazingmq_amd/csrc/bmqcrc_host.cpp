@@ -80,7 +80,7 @@ struct DevBuf {
 // Planner + staging scratch for one (device, stream).
 struct Workspace {
     std::mutex mu;
-    DevBuf seg_first, block_sum, seg2msg, seginfo, bhist, ctrl;
+    DevBuf seg_first, block_sum, segmap, seginfo, bhist, ctrl;
     // host-pointer staging
     DevBuf arena, offsets, lengths, seeds, out;
     // verify / blobs
@@ -187,7 +187,7 @@ int plan_ws(Workspace* w, uint64_t n, uint64_t arena_bytes, uint32_t seg, BatchA
     int rc;
     if ((rc = w->seg_first.ensure(4 * std::max<uint64_t>(n, 1))) ||
         (rc = w->block_sum.ensure(12ull * kPlanMaxBlocks)) ||
-        (rc = w->seg2msg.ensure(4 * max_segs)) || (rc = w->seginfo.ensure(8 * max_segs)) ||
+        (rc = w->segmap.ensure(8 * max_segs)) || (rc = w->seginfo.ensure(8 * max_segs)) ||
         (rc = w->bhist.ensure(4ull * kBuckets * kPlanMaxBlocks)) ||
         (rc = w->ctrl.ensure(sizeof(PlanCtrl)))) {
         return rc;
@@ -198,7 +198,7 @@ int plan_ws(Workspace* w, uint64_t n, uint64_t arena_bytes, uint32_t seg, BatchA
     }
     a->seg_first = (uint32_t*)w->seg_first.p;
     a->block_sum = (uint32_t*)w->block_sum.p;
-    a->seg2msg = (uint32_t*)w->seg2msg.p;
+    a->segmap = (uint32_t*)w->segmap.p;
     a->seginfo = (uint32_t*)w->seginfo.p;
     a->bhist = (uint32_t*)w->bhist.p;
     a->ctrl = (PlanCtrl*)w->ctrl.p;

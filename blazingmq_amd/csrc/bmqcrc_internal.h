@@ -40,7 +40,7 @@ struct BatchArgs {
     uint32_t* out;             // device, n
     uint32_t* seg_first;       // workspace, n: block-local exclusive prefix of segment counts
     uint32_t* block_sum;       // workspace, 3 * nblocks: [sums | non-1 counts | block offsets]
-    uint32_t* seg2msg;         // workspace, max_segs: segment -> message
+    uint32_t* segmap;          // workspace, 2 * max_segs: (message, k) per segment, natural order
     uint32_t* seginfo;         // workspace, 2 * max_segs: (message, k) in size-class order
     uint32_t* bhist;           // workspace, kBuckets * nblocks_seg: histogram, then offsets
     PlanCtrl* ctrl;            // workspace

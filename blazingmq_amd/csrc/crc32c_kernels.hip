@@ -385,8 +385,11 @@ __device__ __forceinline__ SegRef map_segment(const BatchArgs& a, uint32_t seg, 
         } else if (sorted) {
             r.msg = a.seginfo[2u * seg];
             r.k = a.seginfo[2u * seg + 1u];
+        } else if (seg < a.max_segs) {
+            r.msg = a.segmap[2u * seg];
+            r.k = a.segmap[2u * seg + 1u];
         } else {
-            r.msg = seg < a.max_segs ? a.seg2msg[seg] : find_msg(a, seg);
+            r.msg = find_msg(a, seg);  // overflow: past the planned map
             r.k = seg - seg_first_g(a, r.msg);
         }
     }
@@ -661,6 +664,10 @@ __device__ __forceinline__ uint32_t block_scan_1024(uint32_t v, uint32_t* excl, 
 
 // K1: segment counts per message, block-local prefix over the block's
 // contiguous message range, and (last block) the prefix over blocks + totals.
+// Each thread takes kPlanV consecutive messages (a tile = 4096 messages, one
+// block scan) and the next tile's lengths are loaded before the current tile
+// is scanned, so a block pays one load latency, not one per tile.
+constexpr uint32_t kPlanV = 4;
 __global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
 {
     __shared__ uint32_t wsum[40];
@@ -671,38 +678,70 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
         sh[3] = 0;            // max segments per message
     }
     __syncthreads();
+    constexpr uint64_t kTile = (uint64_t)kPlanBlock * kPlanV;
     const uint64_t lo = (uint64_t)blockIdx.x * a.per_msg;
     const uint64_t hi = min(lo + a.per_msg, a.n);
-    uint32_t carry = 0;
-    for (uint64_t base = lo; base < hi; base += kPlanBlock) {
-        const uint64_t i = base + threadIdx.x;
-        uint32_t ns = 0;
-        if (i < hi) {
-            const uint32_t len = a.lengths[i];
-            ns = len ? (len - 1u) / a.seg_bytes + 1u : 0u;
-            a.out[i] = len ? 0u : (a.seeds ? a.seeds[i] : 0u);
-        }
-        // block-level min / max / count(!=1) via wave reductions
-        uint32_t mn = i < hi ? ns : 0xffffffffu, mx = ns;
-        const uint64_t non1 = __ballot(i < hi && ns != 1u);
+    const uint32_t seg = a.seg_bytes;
+    const uint32_t seg_shift = (seg & (seg - 1u)) == 0 ? (uint32_t)__builtin_ctz(seg) : 0u;
+    auto load = [&](uint64_t base, uint32_t (&L)[kPlanV]) {
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
-            mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+        for (uint32_t v = 0; v < kPlanV; ++v) {
+            const uint64_t i = base + (uint64_t)threadIdx.x * kPlanV + v;
+            L[v] = i < hi ? a.lengths[i] : 0u;
         }
-        if ((threadIdx.x & 63) == 0) {
-            atomicMin(&sh[2], mn);
-            atomicMax(&sh[3], mx);
-            if (non1) {
-                atomicAdd(&sh[1], (uint32_t)__popcll(non1));
+    };
+    uint32_t nxt[kPlanV];
+    if (lo < hi) {
+        load(lo, nxt);
+    }
+    uint32_t carry = 0, mn = 0xffffffffu, mx = 0, non1 = 0;
+    for (uint64_t base = lo; base < hi; base += kTile) {
+        uint32_t L[kPlanV];
+#pragma unroll
+        for (uint32_t v = 0; v < kPlanV; ++v) {
+            L[v] = nxt[v];
+        }
+        if (base + kTile < hi) {
+            load(base + kTile, nxt);  // next tile in flight during this scan
+        }
+        uint32_t ns[kPlanV], sum = 0;
+#pragma unroll
+        for (uint32_t v = 0; v < kPlanV; ++v) {
+            const uint64_t i = base + (uint64_t)threadIdx.x * kPlanV + v;
+            const uint32_t len = L[v];
+            ns[v] = len ? (seg_shift ? ((len - 1u) >> seg_shift) : (len - 1u) / seg) + 1u : 0u;
+            if (i < hi) {
+                a.out[i] = len ? 0u : (a.seeds ? a.seeds[i] : 0u);
+                mn = min(mn, ns[v]);
+                mx = max(mx, ns[v]);
+                non1 += ns[v] != 1u ? 1u : 0u;
             }
+            sum += ns[v];
         }
         uint32_t excl;
-        const uint32_t tot = block_scan_1024(ns, &excl, wsum);
-        if (i < hi) {
-            a.seg_first[i] = carry + excl;
+        const uint32_t tot = block_scan_1024(sum, &excl, wsum);
+        uint32_t run = carry + excl;
+#pragma unroll
+        for (uint32_t v = 0; v < kPlanV; ++v) {
+            const uint64_t i = base + (uint64_t)threadIdx.x * kPlanV + v;
+            if (i < hi) {
+                a.seg_first[i] = run;
+            }
+            run += ns[v];
         }
         carry += tot;
+    }
+    // block-level min / max / count(!=1): wave reductions, then LDS atomics
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
+        mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+        non1 += (uint32_t)__shfl_xor((int)non1, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(&sh[2], mn);
+        atomicMax(&sh[3], mx);
+        atomicAdd(&sh[1], non1);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -723,13 +762,13 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
     uint32_t ex;
     const uint32_t total = block_scan_1024(v, &ex, wsum);
     uint32_t ex2;
-    const uint32_t non1 = block_scan_1024(nn, &ex2, wsum);
+    const uint32_t non1_all = block_scan_1024(nn, &ex2, wsum);
     if (j < a.nblocks) {
         a.block_sum[2u * a.nblocks + j] = ex;  // block offsets (read by later launches)
     }
     if (threadIdx.x == 0) {
         a.ctrl->total_segs = total;
-        a.ctrl->identity = (non1 == 0) ? 1u : 0u;
+        a.ctrl->identity = (non1_all == 0) ? 1u : 0u;
         a.ctrl->ngroups = (total + 63u) / 64u;
         a.ctrl->overflow = (total > a.max_segs) ? 1u : 0u;
         a.ctrl->nseg_uniform = (!mismatch && u0 != 0xffffffffu && u0 != 0u) ? u0 : 0u;
@@ -811,7 +850,8 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_emit(BatchArgs a)
                 msg = find_msg(a, (uint32_t)g);  // window exhausted (empty messages)
             }
             const uint32_t k = (uint32_t)g - seg_first_g(a, msg);
-            a.seg2msg[g] = msg;
+            a.segmap[2u * g] = msg;
+            a.segmap[2u * g + 1u] = k;
             atomicAdd(&hist[seg_class(a, msg, k)], 1u);
             if (g + 1 == min(base + kPlanBlock, hi)) {
                 win_lo = msg;  // message of the tile's last segment starts the next window
@@ -896,8 +936,8 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_scatter(BatchArgs a)
         const uint64_t g = base + threadIdx.x;
         uint32_t msg = 0, k = 0, cls = kBuckets;  // kBuckets: no segment
         if (g < hi) {
-            msg = a.seg2msg[g];
-            k = (uint32_t)g - seg_first_g(a, msg);
+            msg = a.segmap[2u * g];
+            k = a.segmap[2u * g + 1u];
             cls = seg_class(a, msg, k);
         }
         uint32_t rank = 0;
