@@ -71,6 +71,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", default="64k_x_64KiB", choices=list(CONFIGS))
     p.add_argument("--seg-bytes", type=int, default=0)
+    p.add_argument("--whole-messages", action="store_true",
+                   help="BMQCRC_F_WHOLE_MESSAGES: one lane per message, no planner launches")
     p.add_argument("--msgs", type=int, default=0,
                    help="experiment: override the message count of a uniform config "
                         "(the line is then marked as not the BASELINE workload)")
@@ -191,7 +193,8 @@ def main():
 
     def step(timed):
         Crc32c.calculate_batch(arena, offsets, lengths, None, out, seg_bytes=args.seg_bytes,
-                               stream=stream, sync=False, time_kernel=timed)
+                               stream=stream, sync=False, time_kernel=timed,
+                               whole_messages=args.whole_messages)
 
     # setup: settle the GPU clocks under this exact load (not part of W or K)
     t_settle = time.perf_counter()
@@ -276,7 +279,8 @@ def main():
             "data": "synthetic (splitmix64 random payload bytes generated in HBM)",
             "config": {"workload": args.config + ": " + desc,
                        "n_msgs_total": n_all, "payload_bytes_total": bytes_all,
-                       "seg_bytes": args.seg_bytes or 16384,
+                       "seg_bytes": args.seg_bytes or "auto",
+                       "whole_messages": bool(args.whole_messages),
                        "parallelism": "dp%d (sharded batch, no collective)" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

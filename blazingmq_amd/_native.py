@@ -18,6 +18,7 @@ BMQCRC_EINVAL = -22
 BMQCRC_F_DEVICE_PTRS = 0x1
 BMQCRC_F_ASYNC = 0x2
 BMQCRC_F_TIME_KERNEL = 0x4
+BMQCRC_F_WHOLE_MESSAGES = 0x8
 
 
 class BmqCrcError(RuntimeError):

@@ -111,14 +111,16 @@ class Crc32c:
 
     @staticmethod
     def calculate_batch(arena, offsets, lengths, seeds=None, out=None, *, seg_bytes=0,
-                        device=None, stream=None, sync=True, time_kernel=False):
+                        device=None, stream=None, sync=True, time_kernel=False,
+                        whole_messages=False):
         """Batched CRC32-C of messages ``arena[offsets[i] : offsets[i]+lengths[i]]``.
 
         torch CUDA tensors: ``arena`` uint8, ``offsets`` int64, ``lengths`` /
         ``seeds`` / ``out`` int32 (read as u32) on one device; the call is
         enqueued on ``stream`` (default: torch's current stream) and
         ``out`` (int32 tensor) is returned.  Host arrays: numpy in, numpy
-        ``uint32`` out.
+        ``uint32`` out.  ``whole_messages`` (BMQCRC_F_WHOLE_MESSAGES): one
+        lane per message, no planner launches -- for batches of small messages.
         """
         try:
             import torch
@@ -126,12 +128,13 @@ class Crc32c:
             torch = None
         if torch is not None and isinstance(arena, torch.Tensor) and arena.is_cuda:
             return _batch_torch(torch, arena, offsets, lengths, seeds, out, seg_bytes, stream,
-                                sync, time_kernel)
-        return _batch_host(arena, offsets, lengths, seeds, out, seg_bytes, device)
+                                sync, time_kernel, whole_messages)
+        return _batch_host(arena, offsets, lengths, seeds, out, seg_bytes, device,
+                           whole_messages)
 
 
 def _batch_torch(torch, arena, offsets, lengths, seeds, out, seg_bytes, stream, sync,
-                 time_kernel=False):
+                 time_kernel=False, whole_messages=False):
     dev = arena.device
     n = offsets.numel()
     for name, t, dt in (("offsets", offsets, torch.int64), ("lengths", lengths, torch.int32)):
@@ -152,6 +155,8 @@ def _batch_torch(torch, arena, offsets, lengths, seeds, out, seg_bytes, stream, 
     flags = _native.BMQCRC_F_DEVICE_PTRS | (0 if sync else _native.BMQCRC_F_ASYNC)
     if time_kernel:
         flags |= _native.BMQCRC_F_TIME_KERNEL
+    if whole_messages:
+        flags |= _native.BMQCRC_F_WHOLE_MESSAGES
     o = _native.make_opts(device=dev.index if dev.index is not None else -1,
                           stream=stream.cuda_stream, flags=flags, seg_bytes=seg_bytes)
     _native.check(_native.lib.bmqcrc_crc32c_batch(
@@ -160,7 +165,7 @@ def _batch_torch(torch, arena, offsets, lengths, seeds, out, seg_bytes, stream, 
     return out
 
 
-def _batch_host(arena, offsets, lengths, seeds, out, seg_bytes, device):
+def _batch_host(arena, offsets, lengths, seeds, out, seg_bytes, device, whole_messages=False):
     a = np.frombuffer(bytes(arena), dtype=np.uint8) if isinstance(
         arena, (bytes, bytearray, memoryview)) else np.ascontiguousarray(arena).view(np.uint8)
     off = np.ascontiguousarray(offsets, dtype=np.uint64)
@@ -169,7 +174,8 @@ def _batch_host(arena, offsets, lengths, seeds, out, seg_bytes, device):
         raise ValueError("offsets/lengths size mismatch")
     sd = None if seeds is None else np.ascontiguousarray(seeds, dtype=np.uint32)
     res = np.empty(off.size, dtype=np.uint32) if out is None else out
-    o = _native.make_opts(device=-1 if device is None else device, seg_bytes=seg_bytes)
+    o = _native.make_opts(device=-1 if device is None else device, seg_bytes=seg_bytes,
+                          flags=_native.BMQCRC_F_WHOLE_MESSAGES if whole_messages else 0)
     _native.check(_native.lib.bmqcrc_crc32c_batch(
         a.ctypes.data if a.size else None, a.size, off.ctypes.data, ln.ctypes.data,
         sd.ctypes.data if sd is not None else None, res.ctypes.data, off.size, ctypes.byref(o)))

@@ -51,8 +51,10 @@ struct BatchArgs {
     uint32_t seg_bytes;
     uint32_t nblocks;          // k_plan blocks (<= kPlanMaxBlocks)
     uint32_t nblocks_seg;      // k_plan_emit / k_plan_scatter blocks (<= kPlanMaxBlocks)
+    uint32_t whole;            // 1: BMQCRC_F_WHOLE_MESSAGES (one segment per message, no planner)
+    uint32_t blocks_per_cu;    // k_fold grid: 1 (large messages) or 2 blocks per CU
     uint32_t tune;             // experiment knobs (BMQCRC_TUNE env): bit0 disables nt LDS-DMA
-                               // loads, bit1 selects a 1-block/CU grid
+                               // loads, bit1 forces a 1-block/CU grid, bit3 forces 2
 };
 
 }  // namespace bmqcrc

@@ -424,10 +424,13 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     }
     __syncthreads();
 
-    const uint32_t total = a.ctrl->total_segs;
-    const uint32_t identity = a.ctrl->identity;
-    const uint32_t sorted = a.ctrl->sorted;
-    const uint32_t uni = a.ctrl->nseg_uniform;
+    // BMQCRC_F_WHOLE_MESSAGES: segment g = message g, one segment each, no
+    // planner ran (ctrl is not read)
+    const uint32_t whole = a.whole;
+    const uint32_t total = whole ? (uint32_t)a.n : a.ctrl->total_segs;
+    const uint32_t identity = whole ? 1u : a.ctrl->identity;
+    const uint32_t sorted = whole ? 0u : a.ctrl->sorted;
+    const uint32_t uni = whole ? 0u : a.ctrl->nseg_uniform;
     const uint32_t ngroups = (total + 63u) / 64u;
     const uint32_t SEG = a.seg_bytes;
     const uint64_t arena = (uint64_t)(uintptr_t)a.arena;
@@ -464,7 +467,8 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         const uint32_t msg = cur.msg, k = cur.k, len = cur.len, seed = cur.seed;
         const uint64_t off = cur.off;
         const uint32_t nseg =
-            valid ? (seg_shift ? ((len - 1u) >> seg_shift) : (len - 1u) / SEG) + 1u : 0u;
+            !valid ? 0u
+                   : (whole ? 1u : (seg_shift ? ((len - 1u) >> seg_shift) : (len - 1u) / SEG) + 1u);
         const uint64_t mstart = arena + off;
         const uint64_t mend = mstart + len;
         const SegGeom geo = seg_geom(mstart, len, k, nseg, SEG);
@@ -1118,12 +1122,15 @@ extern "C" int bmqcrc_launch_batch(const BatchArgs* a, void* stream, int num_cus
     if (a->n == 0) {
         return 0;
     }
-    hipLaunchKernelGGL(k_plan, dim3(a->nblocks), dim3(kPlanBlock), 0, s, *a);
-    hipLaunchKernelGGL(k_plan_emit, dim3(a->nblocks_seg), dim3(kPlanBlock), 0, s, *a);
-    hipLaunchKernelGGL(k_plan_scatter, dim3(a->nblocks_seg), dim3(kPlanBlock), 0, s, *a);
+    if (!a->whole) {
+        hipLaunchKernelGGL(k_plan, dim3(a->nblocks), dim3(kPlanBlock), 0, s, *a);
+        hipLaunchKernelGGL(k_plan_emit, dim3(a->nblocks_seg), dim3(kPlanBlock), 0, s, *a);
+        hipLaunchKernelGGL(k_plan_scatter, dim3(a->nblocks_seg), dim3(kPlanBlock), 0, s, *a);
+    }
     const uint64_t max_groups = (a->max_segs + 63) / 64;
     uint64_t grid = (max_groups + kWavesPerBlock - 1) / kWavesPerBlock;
-    const uint64_t cap = (uint64_t)(num_cus > 0 ? num_cus : 256) * (a->tune & 2u ? 1u : 2u);
+    const uint32_t per_cu = (a->tune & 2u) ? 1u : (a->tune & 8u) ? 2u : a->blocks_per_cu;
+    const uint64_t cap = (uint64_t)(num_cus > 0 ? num_cus : 256) * (per_cu ? per_cu : 2u);
     if (grid > cap) {
         grid = cap;
     }

@@ -50,13 +50,19 @@ extern "C" {
 #define BMQCRC_F_DEVICE_PTRS 0x1u /* arena/offsets/lengths/seeds/out are device pointers */
 #define BMQCRC_F_ASYNC 0x2u       /* device ptrs only: return after enqueueing on stream */
 #define BMQCRC_F_TIME_KERNEL 0x4u /* record HIP events around the fold kernel (see bmqcrc_kernel_timing) */
+/* Fold every message in one lane: no segmentation, no planner launches (one
+ * kernel per batch).  For batches of small messages (PUT events, small
+ * journal records): correct for any lengths, but a long message keeps its
+ * whole wave busy for its full length. */
+#define BMQCRC_F_WHOLE_MESSAGES 0x8u
 
 typedef struct bmqcrc_opts {
     uint32_t struct_size; /* sizeof(bmqcrc_opts) */
     int32_t device;       /* HIP device ordinal; -1 = current device */
     void* stream;         /* hipStream_t; NULL = library-owned stream of that device */
     uint32_t flags;       /* BMQCRC_F_* */
-    uint32_t seg_bytes;   /* segment size in bytes, multiple of 128; 0 = default (16384) */
+    uint32_t seg_bytes;   /* segment size in bytes, multiple of 128 in [256, 2^30]; 0 = automatic:
+                             16 KiB, or up to 64 KiB for batches of large messages */
 } bmqcrc_opts;
 
 /* ---- scalar (host CPU) -------------------------------------------------- */

@@ -91,3 +91,23 @@ def test_batch_refuses_without_gpu():
     with pytest.raises(BmqCrcError) as e:
         Crc32c.calculate_batch(np.zeros(64, np.uint8), [0], [64])
     assert e.value.rc == -19
+
+
+def test_batch_rejects_unknown_flags():
+    import ctypes
+    from blazingmq_amd import _native as N
+    a = np.zeros(64, np.uint8)
+    off = np.zeros(1, np.uint64)
+    ln = np.full(1, 64, np.uint32)
+    out = np.zeros(1, np.uint32)
+    o = N.make_opts(flags=0x100)
+    rc = N.lib.bmqcrc_crc32c_batch(a.ctypes.data, a.size, off.ctypes.data, ln.ctypes.data, None,
+                                   out.ctypes.data, 1, ctypes.byref(o))
+    assert rc == N.BMQCRC_EINVAL
+    assert b"flags" in N.lib.bmqcrc_last_error()
+    # the whole-messages flag is known: without a GPU it refuses with ENODEV
+    o = N.make_opts(flags=N.BMQCRC_F_WHOLE_MESSAGES)
+    rc = N.lib.bmqcrc_crc32c_batch(a.ctypes.data, a.size, off.ctypes.data, ln.ctypes.data, None,
+                                   out.ctypes.data, 1, ctypes.byref(o))
+    if N.lib.bmqcrc_device_count() == 0:
+        assert rc == N.BMQCRC_ENODEV

@@ -97,7 +97,7 @@ def test_data_file_fixture(cuda, golden):
     assert [int(x) for x in got] == [r["crc"] for r in df["records"]]
 
 
-@pytest.mark.parametrize("seg_bytes", [256, 384, 1024, 16384])
+@pytest.mark.parametrize("seg_bytes", [256, 384, 1024, 16384, 65536])
 def test_random_vs_oracle(cuda, seg_bytes):
     rng = np.random.default_rng(1234 + seg_bytes)
     arena = rng.integers(0, 256, size=3 << 20, dtype=np.uint8)
@@ -135,6 +135,38 @@ def test_small_ragged_batches(cuda):
         exp = oracle.batch(arena_np, offs, lens, seeds)
         bad = np.nonzero(got != exp)[0]
         assert bad.size == 0, (t, seg, [(int(i), int(offs[i]), int(lens[i])) for i in bad[:5]])
+
+
+@pytest.mark.parametrize("host", [False, True])
+def test_whole_messages_flag(cuda, golden, host):
+    # BMQCRC_F_WHOLE_MESSAGES: one lane per message, no planner -- any lengths
+    # (empty, tiny, line-crossing, and long ones that keep a wave busy)
+    import torch
+    rng = np.random.default_rng(99 + host)
+    arena_np = rng.integers(0, 256, size=3 << 20, dtype=np.uint8)
+    lens = rng.choice([0, 0, 1, 2, 3, 4, 5, 31, 127, 128, 129, 255, 256, 1000, 4096, 16385,
+                       70000, 300000], size=5000).astype(np.uint32)
+    offs = np.array([rng.integers(0, arena_np.size - l + 1) for l in lens], np.int64)
+    seeds = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64).astype(np.uint32)
+    seeds[rng.random(lens.size) < 0.3] = 0
+    exp = oracle.batch(arena_np, offs, lens, seeds, nthreads=8)
+    if host:
+        got = Crc32c.calculate_batch(arena_np, offs, lens, seeds, whole_messages=True)
+    else:
+        got = Crc32c.calculate_batch(
+            torch.from_numpy(arena_np).to(cuda), torch.from_numpy(offs).to(cuda),
+            torch.from_numpy(lens.view(np.int32)).to(cuda),
+            torch.from_numpy(seeds.view(np.int32)).to(cuda),
+            whole_messages=True).cpu().numpy().view(np.uint32)
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, [(int(i), int(offs[i]), int(lens[i])) for i in bad[:8]]
+    # golden vectors, one batch
+    vec = golden["calculate"]
+    blob = b"".join(bytes.fromhex(v["hex"]) for v in vec)
+    o = np.cumsum([0] + [len(bytes.fromhex(v["hex"])) for v in vec])[:-1]
+    ln = np.array([len(bytes.fromhex(v["hex"])) for v in vec], np.uint32)
+    got = Crc32c.calculate_batch(np.frombuffer(blob, np.uint8), o, ln, whole_messages=True)
+    assert got.tolist() == [v["crc"] for v in vec]
 
 
 def test_line_boundary_edges(cuda):
