@@ -5,7 +5,7 @@ The product is the C-ABI library ``lib/libbmqcrc.so`` (HIP kernels for gfx950
 + host dispatcher); this package is its Python host-side mirror.
 """
 from .crc32c import (Blob, BmqCrcError, Crc32c, calculate_batch_multi,  # noqa: F401
-                     device_count, fill_synthetic, kernel_timing)
+                     device_count, fill_synthetic, kernel_timing, reserve)
 
 __all__ = ["Blob", "BmqCrcError", "Crc32c", "calculate_batch_multi", "device_count",
-           "fill_synthetic", "kernel_timing"]
+           "fill_synthetic", "kernel_timing", "reserve"]

@@ -275,5 +275,13 @@ def kernel_timing(device, stream):
     return tot.value, cnt.value
 
 
+def reserve(device, stream, n_msgs, arena_bytes, seg_bytes=0):
+    """Pre-size the workspace of (device, stream) for batches of up to n_msgs
+    messages over arena_bytes (bmqcrc_reserve): afterwards a device-pointer
+    batch of that size allocates nothing, so it can be captured in a graph."""
+    _native.check(_native.lib.bmqcrc_reserve(device, stream.cuda_stream, n_msgs, arena_bytes,
+                                             seg_bytes))
+
+
 def device_count():
     return _native.lib.bmqcrc_device_count()

@@ -1,0 +1,94 @@
+"""Runtime properties of the batch path on the GPU: hipGraph capture after
+bmqcrc_reserve (the launch path allocates and synchronizes nothing), and
+concurrent batches on different streams from different host threads
+(per-(device, stream) workspaces, bmqp_crc32c.h:40-42 thread safety)."""
+import threading
+
+import numpy as np
+import pytest
+
+import oracle
+from blazingmq_amd import Crc32c, reserve
+
+pytestmark = pytest.mark.gpu
+
+
+def _batch(rng, n, max_len, arena_size):
+    lens = rng.integers(0, max_len, size=n).astype(np.uint32)
+    offs = np.array([rng.integers(0, arena_size - l + 1) for l in lens], np.int64)
+    seeds = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    return offs, lens, seeds
+
+
+@pytest.mark.parametrize("whole", [False, True])
+def test_graph_capture_and_replay(cuda, whole):
+    import torch
+    rng = np.random.default_rng(31 + whole)
+    size = 8 << 20
+    arena_np = rng.integers(0, 256, size=size, dtype=np.uint8)
+    offs, lens, seeds = _batch(rng, 3000, 40000, size)
+    arena = torch.from_numpy(arena_np).to(cuda)
+    o = torch.from_numpy(offs).to(cuda)
+    ln = torch.from_numpy(lens.view(np.int32)).to(cuda)
+    sd = torch.from_numpy(seeds.view(np.int32)).to(cuda)
+    out = torch.zeros(lens.size, dtype=torch.int32, device=cuda)
+    side = torch.cuda.Stream(cuda)
+    reserve(cuda.index or 0, side, lens.size, size)
+    # warm the workspace on the capture stream, then capture one batch
+    with torch.cuda.stream(side):
+        Crc32c.calculate_batch(arena, o, ln, sd, out, stream=side, sync=False,
+                               whole_messages=whole)
+    side.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        Crc32c.calculate_batch(arena, o, ln, sd, out, stream=side, sync=False,
+                               whole_messages=whole)
+    for it in range(3):  # replays read the arena as it is at replay time
+        new = rng.integers(0, 256, size=size, dtype=np.uint8)
+        arena.copy_(torch.from_numpy(new).to(cuda))
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, oracle.batch(new, offs, lens, seeds, nthreads=8)), it
+
+
+def test_concurrent_streams_and_threads(cuda):
+    import torch
+    rng = np.random.default_rng(41)
+    size = 16 << 20
+    jobs = []
+    for t in range(4):
+        arena_np = rng.integers(0, 256, size=size, dtype=np.uint8)
+        offs, lens, seeds = _batch(rng, 20000 if t % 2 else 400, 1 << 16 if t % 2 else 200000,
+                                   size)
+        jobs.append((arena_np, offs, lens, seeds))
+    results = [None] * len(jobs)
+    errors = []
+
+    def work(i):
+        try:
+            arena_np, offs, lens, seeds = jobs[i]
+            s = torch.cuda.Stream(cuda)
+            with torch.cuda.stream(s):
+                arena = torch.from_numpy(arena_np).to(cuda, non_blocking=False)
+                o = torch.from_numpy(offs).to(cuda)
+                ln = torch.from_numpy(lens.view(np.int32)).to(cuda)
+                sd = torch.from_numpy(seeds.view(np.int32)).to(cuda)
+                outs = [Crc32c.calculate_batch(arena, o, ln, sd, stream=s, sync=False)
+                        for _ in range(5)]
+            s.synchronize()
+            results[i] = [x.cpu().numpy().view(np.uint32) for x in outs]
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    threads = [threading.Thread(target=work, args=(i,)) for i in range(len(jobs))]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    assert not errors, errors
+    for (arena_np, offs, lens, seeds), res in zip(jobs, results):
+        exp = oracle.batch(arena_np, offs, lens, seeds, nthreads=8)
+        for r in res:
+            assert np.array_equal(r, exp)
