@@ -12,6 +12,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <fstream>
+#include <iterator>
 #include <random>
 #include <string>
 #include <thread>
@@ -336,6 +338,67 @@ static void gpu_protocol(const std::vector<std::string>& apps, std::string ev, s
              BMQCRC_CSL_INVALID_CHECKSUM);
 }
 
+// The reference's on-disk fixture (bmqstoragetool integration data, copied
+// to tests/golden/): two MESSAGE records whose app data "hello world" has
+// CRC32-C 3381945770 (detail_result.txt:15,53), journal offsets 224 and 644.
+static bool read_file(const std::string& path, std::string* out)
+{
+    std::ifstream f(path, std::ios::binary);
+    if (!f) {
+        return false;
+    }
+    out->assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
+    return true;
+}
+
+static bool fixture(std::string* journal, std::string* data)
+{
+    const char* dir = getenv("BMQCRC_GOLDEN_DIR");
+    if (!dir) {
+        return false;
+    }
+    const bool ok = read_file(std::string(dir) + "/test.bmq_journal", journal) &&
+                    read_file(std::string(dir) + "/test.bmq_data", data);
+    if (!ok) {
+        fprintf(stderr, "fixture: cannot read %s\n", dir);
+        ++g_fail;
+    }
+    return ok;
+}
+
+static void recovery_scan(const std::string& j, const std::string& d)
+{
+    uint64_t rec[4], off[4];
+    uint32_t len[4], crc[4];
+    CHECK_EQ(bmqcrc_journal_scan(j.data(), j.size(), d.data(), d.size(), rec, off, len, crc, 4),
+             2);
+    CHECK_EQ(rec[0], 224u);
+    CHECK_EQ(rec[1], 644u);
+    for (int i = 0; i < 2; ++i) {
+        CHECK_EQ(len[i], 11u);
+        CHECK_EQ(crc[i], 3381945770u);
+        CHECK_EQ(memcmp(d.data() + off[i], "hello world", 11), 0);
+        CHECK_EQ(Crc32c::calculate(d.data() + off[i], len[i]), 3381945770u);
+    }
+}
+
+static void gpu_recovery(const std::string& j, std::string d)
+{
+    using namespace BloombergLP;
+    uint64_t n = 0, bad = 0, where[2] = {0, 0};
+    CHECK_EQ(mqbs::FileStoreCrc32c::verifyRecovery(j.data(), j.size(), d.data(), d.size(), &n,
+                                                   &bad, where, 2),
+             0);
+    CHECK_EQ(n, 2u);
+    CHECK_EQ(bad, 0u);
+    d[76 + 4] ^= 0x20;  // second record's app data: "hello World"
+    CHECK_EQ(mqbs::FileStoreCrc32c::verifyRecovery(j.data(), j.size(), d.data(), d.size(), &n,
+                                                   &bad, where, 2),
+             0);
+    CHECK_EQ(bad, 1u);
+    CHECK_EQ(where[0], 644u);
+}
+
 static void gpu_batch()
 {
     if (bmqcrc_device_count() <= 0) {
@@ -402,9 +465,17 @@ int main(int argc, char** argv)
     std::vector<std::string> apps;
     std::string ev, log;
     protocol_scans(&apps, &ev, &log);
+    std::string journal, data;
+    const bool have_fixture = fixture(&journal, &data);
+    if (have_fixture) {
+        recovery_scan(journal, data);
+    }
     if (argc > 1 && strcmp(argv[1], "gpu") == 0) {
         gpu_batch();
         gpu_protocol(apps, ev, log);
+        if (have_fixture) {
+            gpu_recovery(journal, data);
+        }
     } else {
         // without a GPU the batch path must refuse loudly, never fall back
         unsigned out = 0;

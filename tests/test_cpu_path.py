@@ -80,7 +80,8 @@ def test_cpp_dropin_selftest():
     exe = os.path.join(ROOT, "tests", "cpp", "bin", "bmqp_selftest")
     if not os.path.exists(exe):
         pytest.skip("selftest not built")
-    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    env = dict(os.environ, BMQCRC_GOLDEN_DIR=os.path.join(ROOT, "tests", "golden"))
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "PASS" in r.stdout
 

@@ -307,5 +307,6 @@ def test_cpp_dropin_gpu_batch(cuda):
     import os
     import subprocess
     exe = os.path.join(os.path.dirname(__file__), "cpp", "bin", "bmqp_selftest")
-    r = subprocess.run([exe, "gpu"], capture_output=True, text=True, timeout=300)
+    env = dict(os.environ, BMQCRC_GOLDEN_DIR=os.path.join(os.path.dirname(__file__), "golden"))
+    r = subprocess.run([exe, "gpu"], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0 and "PASS" in r.stdout, r.stdout + r.stderr
