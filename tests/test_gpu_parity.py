@@ -217,6 +217,23 @@ def test_overlapping_messages(cuda):
     assert np.array_equal(got, exp)
 
 
+def test_overlapping_ragged_overflow(cuda):
+    # Ragged messages that overlap so much that the segment count exceeds the
+    # planner's map (n + arena/seg): segments past it are resolved by binary
+    # search over the prefix in the fold (the overflow path).
+    rng = np.random.default_rng(14)
+    arena = rng.integers(0, 256, size=1 << 16, dtype=np.uint8)
+    n = 3000
+    lens = rng.integers(0, 60000, size=n)
+    offs = np.array([rng.integers(0, arena.size - l + 1) for l in lens], np.int64)
+    segs = int(((lens + 511) // 512).sum())
+    assert segs > n + arena.size // 512 + 64  # really past the map
+    got = _dev_batch(cuda, arena, offs, lens, seg_bytes=512)
+    exp = oracle.batch(arena, offs, lens, nthreads=8)
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, [(int(i), int(offs[i]), int(lens[i])) for i in bad[:8]]
+
+
 def test_fill_matches_oracle_stream(cuda):
     import torch
     from blazingmq_amd import fill_synthetic
