@@ -87,8 +87,17 @@ struct Workspace {
     DevBuf expected, vcount, vidx, vblock, buf_crc, first_buf;
     // BMQCRC_F_TIME_KERNEL: event pairs around k_fold not yet reported
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timing, spare;
+    // Shape of the last batch planned on this workspace, written by k_fold
+    // into host-mapped memory (kHint*): after a closed-form batch the next
+    // one skips the k_plan_emit/k_plan_scatter launches.  A wrong guess only
+    // costs speed (k_fold then maps segments by binary search).
+    uint32_t* hint_host = nullptr;
+    uint32_t* hint_dev = nullptr;
     ~Workspace()
     {
+        if (hint_host) {
+            (void)hipHostFree(hint_host);
+        }
         for (auto& v : {timing, spare}) {
             for (auto& e : v) {
                 (void)hipEventDestroy(e.first);
@@ -196,6 +205,22 @@ int plan_ws(Workspace* w, uint64_t n, uint64_t arena_bytes, uint32_t seg, BatchA
         // last-block-done tickets must start at zero (the kernels reset them)
         HIP_TRY(hipMemset(w->ctrl.p, 0, w->ctrl.bytes));
     }
+    if (!w->hint_host) {
+        void* h = nullptr;
+        HIP_TRY(hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocPortable |
+                                          hipHostMallocCoherent));
+        *(volatile uint32_t*)h = kHintUnknown;
+        void* d = nullptr;
+        const hipError_t e = hipHostGetDevicePointer(&d, h, 0);
+        if (e != hipSuccess) {
+            (void)hipHostFree(h);
+            return fail(BMQCRC_EIO, std::string("hipHostGetDevicePointer: ") + hipGetErrorString(e));
+        }
+        w->hint_host = (uint32_t*)h;
+        w->hint_dev = (uint32_t*)d;
+    }
+    a->shape_hint = w->hint_dev;
+    a->map_planned = 1;
     a->seg_first = (uint32_t*)w->seg_first.p;
     a->block_sum = (uint32_t*)w->block_sum.p;
     a->segmap = (uint32_t*)w->segmap.p;
@@ -282,6 +307,9 @@ int run_batch(Ctx& c, uint32_t flags, uint32_t seg, const void* arena, uint64_t 
         a.max_segs = n;
     } else if ((rc = plan_ws(w, n, arena_bytes, seg, &a))) {
         return rc;
+    } else if (!(tune & 16u) &&
+               __atomic_load_n(w->hint_host, __ATOMIC_RELAXED) == kHintClosed) {
+        a.map_planned = 0;  // last batch was closed-form: predict this one is too
     }
     a.arena = (const uint8_t*)arena;
     a.offsets = offsets;

@@ -54,8 +54,19 @@ struct BatchArgs {
     uint32_t whole;            // 1: BMQCRC_F_WHOLE_MESSAGES (one segment per message, no planner)
     uint32_t blocks_per_cu;    // k_fold grid: 1 (large messages) or 2 blocks per CU
     uint32_t tune;             // experiment knobs (BMQCRC_TUNE env): bit0 disables nt LDS-DMA
-                               // loads, bit1 forces a 1-block/CU grid, bit3 forces 2
+                               // loads, bit1 forces a 1-block/CU grid, bit3 forces 2, bit4
+                               // always launches k_plan_emit/k_plan_scatter
+    uint32_t map_planned;      // 1: k_plan_emit/k_plan_scatter run before k_fold; 0: they
+                               //    were skipped (the previous batch on this workspace was
+                               //    closed-form) and a ragged batch maps segments by binary
+                               //    search instead -- slower, never wrong
+    uint32_t* shape_hint;      // host-mapped word or nullptr: k_fold writes kHintClosed or
+                               // kHintRagged, the host reads it when planning the next batch
 };
+
+constexpr uint32_t kHintUnknown = 0;
+constexpr uint32_t kHintClosed = 1;  // identity or uniform segment counts
+constexpr uint32_t kHintRagged = 2;
 
 }  // namespace bmqcrc
 

@@ -14,13 +14,21 @@
 //     32-word register ring -- 9 v_bitop3 (3-input XOR) per word, no
 //     carry-less multiply, no lookup table.
 //   * Only the last 32 remainder words get a real GF(2) reduction (Horner by
-//     x^32, 64 VALU/word), once per segment.
+//     x^32 with slicing tables in LDS), once per segment.
 //   * Bytes reach the lanes through LDS: per round a wave DMAs (LDS-DMA,
 //     global_load_lds_dwordx4) the next 128-byte line of each of its 64
 //     segments, 8 lanes per full 128-byte line (coalesced), with the piece
 //     order XOR-swizzled on the SOURCE address so that every owner lane's
-//     ds_read_b128 is bank-conflict free.  Two LDS slots per wave: round r+1
-//     is in flight while round r folds.
+//     ds_read_b128 is bank-conflict free.  Pieces outside a segment's bytes
+//     are read from a zero line instead, so only the 16-byte pieces cut by a
+//     segment's first or last byte need a byte mask (a few LDS
+//     read-modify-writes).  Two LDS slots per wave: round r+1 is in flight
+//     while round r folds (one slot in the 4-blocks-per-CU variant).
+//   * Streams are right-aligned in the wave: a lane with nl lines starts at
+//     round R - nl (R = the wave's longest stream) and folds zero lines
+//     before that, which leaves a zero-init CRC unchanged.  Every lane thus
+//     ends in round R-1 and the remainder reduction runs once per wave, not
+//     once per distinct segment length.
 //   * Per-segment raw remainders are moved to the message end with x^e mod P
 //     (e mod ord(x) = 2^31-1, which also un-shifts the zero padding) and
 //     XOR-combined into out[msg] (plain store for single-segment messages,
@@ -38,12 +46,17 @@
 namespace bmqcrc {
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const u32x4 lds_cu4;
 
 __constant__ uint32_t c_x2col[31][32] = BMQCRC_X2COL;
 __constant__ uint32_t c_xneg8[136] = BMQCRC_XNEG8;
 __constant__ uint32_t c_ty[8][256] = BMQCRC_TY;
+
+// All-zero line in device memory: the LDS-DMA source of every 16-byte piece
+// that lies outside a segment's bytes, and of every round outside its stream.
+__device__ __attribute__((aligned(128))) uint8_t g_zero_line[128];
 
 // ------------------------------------------------------------ GF(2) helpers
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
@@ -134,13 +147,6 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src)
     return ((uint64_t)hi << 32) | lo;
 }
 
-__device__ __forceinline__ uint64_t rfl64(uint64_t v)
-{
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    return ((uint64_t)hi << 32) | lo;
-}
-
 // ---------------------------------------------------- fold ring (m(y) taps)
 constexpr int kTaps[BMQCRC_REL_NTAPS] = BMQCRC_REL_TAPS;
 constexpr int kNTaps = BMQCRC_REL_NTAPS;
@@ -175,8 +181,7 @@ __device__ __forceinline__ void fold_round(uint32_t (&q)[32], const uint32_t (&m
 //   c <- (c ^ R_d) * y^2  ^  R_{d+1} * y
 __device__ __forceinline__ uint32_t tab_lookup(uint32_t tab_lds, int k, uint32_t b)
 {
-    return *(const __attribute__((address_space(3))) uint32_t*)(uintptr_t)(tab_lds + k * 1024u +
-                                                                           b * 4u);
+    return *(const lds_u32*)(uintptr_t)(tab_lds + k * 1024u + b * 4u);
 }
 
 __device__ __forceinline__ uint32_t tail_round(const uint32_t (&q)[32], const uint32_t (&m)[32],
@@ -221,41 +226,56 @@ __device__ __forceinline__ uint32_t tail_round(const uint32_t (&q)[32], const ui
     return c;
 }
 
-// Byte masks of a 128-byte line, branch-free: each word compares its
-// (compile-time) index with the lane's cut word and selects, ~5 VALU/word.
-// Zero bytes [0, sR) (sR in [0, 127]; sR = 0 leaves the line unchanged).
-__device__ __forceinline__ void mask_lo(uint32_t (&m)[32], int sR)
+// Word w (0..31) of this lane's 128-byte line in an LDS slot (the pieces are
+// XOR-swizzled; rd_off is the lane's swizzled line base, see k_fold).
+__device__ __forceinline__ lds_u32* line_word(uint32_t slot, uint32_t rd_off, uint32_t w)
 {
-    const int qs = sR >> 2;
-    const uint32_t part = 0xffffffffu << (8 * (sR & 3));
-#pragma unroll
-    for (int d = 0; d < 32; ++d) {
-        m[d] = (d < qs) ? 0u : ((d == qs) ? (m[d] & part) : m[d]);
-    }
+    return (lds_u32*)(uintptr_t)(slot + (rd_off ^ (16u * (w >> 2))) + 4u * (w & 3u));
 }
 
-// Zero bytes [eR, 128) (eR in [0, 128]; 128 leaves the line unchanged).
-__device__ __forceinline__ void mask_hi(uint32_t (&m)[32], int eR)
+// Byte-exact edges of a lane's line, fixed in LDS before the line is read
+// into registers.  The DMA has already substituted zeros for every 16-byte
+// piece outside the segment's bytes [S, E); what remains are the (at most two)
+// pieces cut by S or E and the seed word:
+//   lo: zero bytes [16*floor(s/16), s) of the line (s = S's offset, s % 16 != 0);
+//   hi: zero bytes [e, 16*ceil(e/16))              (e = E's offset, e % 16 != 0);
+//   sd: XOR ~seed into bytes [sr, sr+4) (sr in [-3, 127]: the word may begin in
+//       the previous line or run into the next one), after the zeroing, so a
+//       message shorter than 4 bytes gets its seed over zeros.
+// A few LDS read-modify-writes per cut line replace whole-line register masks
+// (~170 VALU each, once per distinct cut round of the wave).
+__device__ void line_fixup(uint32_t slot, uint32_t rd_off, bool lo, uint32_t s, bool hi,
+                           uint32_t e, bool sd, int sr, uint32_t c0)
 {
-    const int qe = eR >> 2;
-    const uint32_t part = (eR & 3) ? (0xffffffffu >> (32 - 8 * (eR & 3))) : 0u;
-#pragma unroll
-    for (int d = 0; d < 32; ++d) {
-        m[d] = (d > qe) ? 0u : ((d == qe) ? (m[d] & part) : m[d]);
+    if (lo) {
+        const uint32_t ws = s >> 2;
+        for (uint32_t w = (s >> 4) << 2; w < ws; ++w) {
+            *line_word(slot, rd_off, w) = 0u;
+        }
+        if (s & 3u) {
+            lds_u32* p = line_word(slot, rd_off, ws);
+            *p &= 0xffffffffu << (8u * (s & 3u));
+        }
     }
-}
-
-// XOR the seed word c0 into bytes [sR, sR+4) of the line (sR in [-3, 127]:
-// the word may start in the previous line; sR = -64 leaves the line unchanged).
-__device__ __forceinline__ void inject_seed(uint32_t (&m)[32], int sR, uint32_t c0)
-{
-    const int qs = sR >> 2;  // floor
-    const int sh = 8 * (sR & 3);
-    const uint32_t lo = c0 << sh;
-    const uint32_t hi = sh ? (c0 >> (32 - sh)) : 0u;
-#pragma unroll
-    for (int d = 0; d < 32; ++d) {
-        m[d] ^= (d == qs) ? lo : ((d == qs + 1) ? hi : 0u);
+    if (hi) {
+        const uint32_t we = e >> 2;
+        lds_u32* p = line_word(slot, rd_off, we);
+        *p &= (e & 3u) ? (0xffffffffu >> (32u - 8u * (e & 3u))) : 0u;
+        for (uint32_t w = we + 1u; w < (((e >> 4) + 1u) << 2); ++w) {
+            *line_word(slot, rd_off, w) = 0u;
+        }
+    }
+    if (sd) {
+        const int qs = sr >> 2;  // floor
+        const uint32_t sh = 8u * ((uint32_t)sr & 3u);
+        if (qs >= 0) {
+            lds_u32* p = line_word(slot, rd_off, (uint32_t)qs);
+            *p ^= c0 << sh;
+        }
+        if (sh && qs + 1 < 32) {
+            lds_u32* p = line_word(slot, rd_off, (uint32_t)(qs + 1));
+            *p ^= c0 >> (32u - sh);
+        }
     }
 }
 
@@ -290,18 +310,20 @@ __device__ __forceinline__ void inject_seed(uint32_t (&m)[32], int sR, uint32_t 
     "global_load_lds_dwordx4 %9, off" CP "\n\t"                                             \
     "s_mov_b32 m0, %0\n\t"
 
-// Lanes whose segment has no line r (finished, or none) all read one dummy
-// line shared by the wave, so ragged waves add ~1 line per instruction of
-// traffic instead of re-reading every finished segment's last line.
+// Instruction i carries piece pp_i of segment 8i + lane/8.  The piece's index
+// in that segment's stream in round r is 8r - plo[i]; it is read from HBM when
+// that index lies in [0, pcnt[i]) (the piece overlaps the segment's bytes) and
+// from the zero line otherwise (before the lane's stream starts, after its
+// data ends, or a piece wholly outside [S, E)).
 template <bool NT>
-__device__ __forceinline__ void dma_round(uint32_t lds_dst, const uint64_t (&dbase)[8],
-                                          const uint32_t (&nlines)[8], uint64_t dummy,
-                                          uint32_t r)
+__device__ __forceinline__ void dma_round(uint32_t lds_dst, const uint64_t (&pbase)[8],
+                                          const uint32_t (&plo)[8], const uint32_t (&pcnt)[8],
+                                          uint64_t zero, uint32_t r)
 {
     uint64_t s[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        s[i] = (r < nlines[i]) ? dbase[i] + ((uint64_t)r << 7) : dummy;
+        s[i] = (8u * r - plo[i] < pcnt[i]) ? pbase[i] + ((uint64_t)r << 7) : zero;
     }
     uint32_t keep;
     if (NT) {
@@ -385,11 +407,11 @@ __device__ __forceinline__ SegRef map_segment(const BatchArgs& a, uint32_t seg, 
         } else if (sorted) {
             r.msg = a.seginfo[2u * seg];
             r.k = a.seginfo[2u * seg + 1u];
-        } else if (seg < a.max_segs) {
+        } else if (a.map_planned && seg < a.max_segs) {
             r.msg = a.segmap[2u * seg];
             r.k = a.segmap[2u * seg + 1u];
         } else {
-            r.msg = find_msg(a, seg);  // overflow: past the planned map
+            r.msg = find_msg(a, seg);  // no map (skipped or overflow): binary search
             r.k = seg - seg_first_g(a, r.msg);
         }
     }
@@ -407,20 +429,22 @@ __device__ __forceinline__ SegDesc fetch_desc(const BatchArgs& a, SegRef r, bool
     return d;
 }
 
-template <bool NT>
-__global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
+// SLOTS = LDS ring depth per wave: 2 (two 4-wave blocks per CU, or one for
+// large-message batches) or 1 (three blocks per CU: 40 KiB of LDS each).
+template <bool NT, int SLOTS>
+__global__ __launch_bounds__(256, SLOTS == 1 ? 3 : 2) void k_fold(BatchArgs a)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kTabBytes + kLdsBytes];
+    __shared__ __attribute__((aligned(16)))
+    uint8_t lds[kTabBytes + kWavesPerBlock * SLOTS * kSlotBytes];
 
     const int lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t tab_lds = (uint32_t)(uintptr_t)(lds_u8*)lds;
-    const uint32_t wave_lds = tab_lds + kTabBytes + wave * (kSlots * kSlotBytes);
+    const uint32_t wave_lds = tab_lds + kTabBytes + wave * (SLOTS * kSlotBytes);
 
     // remainder-reduction tables -> LDS (8 KiB, once per block; no DMA in flight yet)
     for (uint32_t t = threadIdx.x; t < 8u * 256u; t += blockDim.x) {
-        *(__attribute__((address_space(3))) uint32_t*)(uintptr_t)(tab_lds + 4u * t) =
-            c_ty[t >> 8][t & 255u];
+        *(lds_u32*)(uintptr_t)(tab_lds + 4u * t) = c_ty[t >> 8][t & 255u];
     }
     __syncthreads();
 
@@ -434,8 +458,14 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     const uint32_t ngroups = (total + 63u) / 64u;
     const uint32_t SEG = a.seg_bytes;
     const uint64_t arena = (uint64_t)(uintptr_t)a.arena;
+    if (a.shape_hint && blockIdx.x == 0 && threadIdx.x == 0 && !whole) {
+        // batch shape for the host's next launch decision (host-mapped word)
+        __hip_atomic_store(a.shape_hint, (identity || uni) ? kHintClosed : kHintRagged,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 
     const uint32_t rd_off = (uint32_t)lane * 128u + (((uint32_t)lane >> 1) & 7u) * 16u;
+    const uint64_t zero = (uint64_t)(uintptr_t)g_zero_line + 16u * ((uint32_t)lane & 7u);
 
     const uint32_t stride = gridDim.x * kWavesPerBlock;
     const uint32_t seg_shift = (SEG & (SEG - 1u)) == 0 ? (uint32_t)__builtin_ctz(SEG) : 0u;
@@ -472,24 +502,36 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         const uint64_t mstart = arena + off;
         const uint64_t mend = mstart + len;
         const SegGeom geo = seg_geom(mstart, len, k, nseg, SEG);
-        const uint64_t S = geo.S, E = geo.E, L0 = geo.L0;
+        const uint64_t E = geo.E, L0 = geo.L0;
         const bool first = valid && k == 0;
         const uint32_t nl = valid ? geo.nl : 0u;
-        const uint32_t nl_data = valid ? geo.nl_data : 0u;
-        const uint32_t R = wave_max(nl);
+        const uint32_t R = wave_max(nl);  // lane 0 always holds a valid segment here: R >= 1
+        // right-aligned stream: this lane's line j is round r0 + j
+        const uint32_t r0 = R - nl;
+        const uint32_t sl = valid ? (uint32_t)(geo.S - L0) : 0u;  // S's offset in line 0
+        const uint64_t el = valid ? E - L0 : 0u;                  // E's offset in the stream
+        const bool lo_part = (sl & 15u) != 0;
+        const bool hi_part = (el & 15u) != 0;
+        const uint32_t jE = (uint32_t)(el >> 7);    // line holding E's cut piece
+        const uint32_t eE = (uint32_t)(el & 127u);  // E's offset in that line
 
         // ------------------------------------------ DMA source per instruction
-        // lane 0 always holds a valid segment here; its first line is the dummy
-        const uint64_t dummy = rfl64(L0) + 16u * ((uint32_t)lane & 7u);
-        uint64_t dbase[8];
-        uint32_t dlim[8];  // lines of data of segment 8i + lane/8 (0: none)
+        // pieces [gS, gE) of the stream overlap [S, E); the stream piece index
+        // in round r is 8 (r - r0) + piece
+        const uint32_t gS = sl >> 4;
+        const uint32_t gE = (uint32_t)((el + 15u) >> 4);
+        const uint32_t plo_l = 8u * r0 + gS;
+        const uint32_t pcnt_l = valid ? gE - gS : 0u;
+        const uint64_t pb_l = L0 - ((uint64_t)r0 << 7);
+        uint64_t pbase[8];
+        uint32_t plo[8], pcnt[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int src = 8 * i + (lane >> 3);
-            const uint64_t l0 = shfl64(L0, src);
-            const uint32_t p = ((uint32_t)lane & 7u) ^ ((4u * i + ((uint32_t)lane >> 4)) & 7u);
-            dbase[i] = l0 + 16u * p;
-            dlim[i] = (uint32_t)__shfl((int)nl_data, src);
+            const uint32_t pp = ((uint32_t)lane & 7u) ^ ((4u * i + ((uint32_t)lane >> 4)) & 7u);
+            pbase[i] = shfl64(pb_l, src) + 16u * pp;
+            plo[i] = (uint32_t)__shfl((int)plo_l, src) - pp;
+            pcnt[i] = (uint32_t)__shfl((int)pcnt_l, src);
         }
 
         // ------------------------------------------------------ fold rounds
@@ -500,18 +542,31 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         }
         uint32_t crc = 0;
         const uint32_t c0 = ~seed;
-        const uint64_t inj_end = first ? S + 4 : S;
 
-        dma_round<NT>(wave_lds, dbase, dlim, dummy, 0);
-        if (R > 1) {
-            dma_round<NT>(wave_lds + kSlotBytes, dbase, dlim, dummy, 1);
+        dma_round<NT>(wave_lds, pbase, plo, pcnt, zero, 0);
+        if (SLOTS == 2 && R > 1) {
+            dma_round<NT>(wave_lds + kSlotBytes, pbase, plo, pcnt, zero, 1);
         }
         for (uint32_t r = 0; r < R; ++r) {
-            const uint32_t slot = wave_lds + (r & 1u) * kSlotBytes;
-            if (r + 1 < R) {
+            const uint32_t slot = wave_lds + (SLOTS == 2 ? (r & 1u) * kSlotBytes : 0u);
+            if (SLOTS == 2 && r + 1 < R) {
                 asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
             } else {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            // Byte edges of this round's line: the piece cut by S (first line),
+            // the piece cut by E, and the seed word (first segment only; it may
+            // spill into the second line).  Lanes before their stream (j wraps)
+            // match none of these.
+            const uint32_t j = r - r0;
+            const bool fx_lo = lo_part && j == 0u;
+            const bool fx_hi = hi_part && j == jE;
+            const bool fx_sd = first && (j == 0u || (j == 1u && sl > 124u));
+            if (__ballot(fx_lo || fx_hi || fx_sd)) {
+                if (fx_lo || fx_hi || fx_sd) {
+                    line_fixup(slot, rd_off, fx_lo, sl, fx_hi, eE, fx_sd, (int)(sl - 128u * j),
+                               c0);
+                }
             }
             uint32_t m[32];
 #pragma unroll
@@ -522,31 +577,13 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
                 m[4 * kk + 2] = v.z;
                 m[4 * kk + 3] = v.w;
             }
-            if (r + 2 < R) {
-                dma_round<NT>(slot, dbase, dlim, dummy, r + 2);
+            if (r + SLOTS < R) {
+                dma_round<NT>(slot, pbase, plo, pcnt, zero, r + SLOTS);
             }
-            // Zero the bytes outside [S, E) and XOR the seed word in at S; each
-            // step runs only when some lane of the wave needs it this round.
-            const uint64_t p0 = L0 + ((uint64_t)r << 7);
-            const bool live = r < nl;
-            const bool lo_cut = live && p0 < S;           // first line, unaligned start
-            const bool hi_cut = live && p0 + 128u > E;    // last line(s): bytes from E on
-            const bool inj = live && p0 < inj_end && S < p0 + 128u;  // seed word here
-            if (__ballot(lo_cut)) {
-                mask_lo(m, lo_cut ? (int)(S - p0) : 0);
-            }
-            if (__ballot(hi_cut)) {
-                mask_hi(m, hi_cut ? (int)(E > p0 ? E - p0 : 0) : 128);
-            }
-            if (__ballot(inj && S != p0)) {
-                inject_seed(m, inj ? (int)((int64_t)S - (int64_t)p0) : -64, c0);
-            } else if (inj) {
-                m[0] ^= c0;  // line-aligned message start: the seed is word 0
-            }
-            if (r + 1 < nl) {
+            if (r + 1 < R) {
                 fold_round(q, m);
-            } else if (r + 1 == nl) {
-                crc = tail_round(q, m, tab_lds);
+            } else {
+                crc = tail_round(q, m, tab_lds);  // every lane's last line: one tail per wave
             }
         }
 
@@ -567,9 +604,6 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         if (first) {
             contrib ^= 0xffffffffu;
         }
-        // XOR-reduce the runs of lanes that hold segments of the same message
-        // (segments of a message are consecutive), then one store or atomic
-        // per run: the run head owns the result.
         // XOR-reduce each run of adjacent lanes holding the same message, then
         // one store or atomic per run: the run head owns the result.  A
         // message may occupy several runs of one wave (the size-class sort
@@ -1124,12 +1158,17 @@ extern "C" int bmqcrc_launch_batch(const BatchArgs* a, void* stream, int num_cus
     }
     if (!a->whole) {
         hipLaunchKernelGGL(k_plan, dim3(a->nblocks), dim3(kPlanBlock), 0, s, *a);
-        hipLaunchKernelGGL(k_plan_emit, dim3(a->nblocks_seg), dim3(kPlanBlock), 0, s, *a);
-        hipLaunchKernelGGL(k_plan_scatter, dim3(a->nblocks_seg), dim3(kPlanBlock), 0, s, *a);
+        if (a->map_planned) {
+            hipLaunchKernelGGL(k_plan_emit, dim3(a->nblocks_seg), dim3(kPlanBlock), 0, s, *a);
+            hipLaunchKernelGGL(k_plan_scatter, dim3(a->nblocks_seg), dim3(kPlanBlock), 0, s, *a);
+        }
     }
+    // tune bit5: one LDS slot per wave, three blocks per CU (3 waves per SIMD)
+    const bool one_slot = (a->tune & 32u) != 0;
     const uint64_t max_groups = (a->max_segs + 63) / 64;
     uint64_t grid = (max_groups + kWavesPerBlock - 1) / kWavesPerBlock;
-    const uint32_t per_cu = (a->tune & 2u) ? 1u : (a->tune & 8u) ? 2u : a->blocks_per_cu;
+    const uint32_t per_cu =
+        one_slot ? 3u : (a->tune & 2u) ? 1u : (a->tune & 8u) ? 2u : a->blocks_per_cu;
     const uint64_t cap = (uint64_t)(num_cus > 0 ? num_cus : 256) * (per_cu ? per_cu : 2u);
     if (grid > cap) {
         grid = cap;
@@ -1140,11 +1179,18 @@ extern "C" int bmqcrc_launch_batch(const BatchArgs* a, void* stream, int num_cus
     if (ev_start) {
         (void)hipEventRecord((hipEvent_t)ev_start, s);
     }
-    if (!(a->tune & 1u)) {  // default: non-temporal LDS-DMA (once-read stream)
-        hipLaunchKernelGGL(k_fold<true>, dim3((unsigned)grid), dim3(kWavesPerBlock * 64), 0, s, *a);
+    const dim3 gd((unsigned)grid), bd(kWavesPerBlock * 64);
+    const bool nt = !(a->tune & 1u);  // default: non-temporal LDS-DMA (once-read stream)
+    if (one_slot) {
+        if (nt) {
+            hipLaunchKernelGGL((k_fold<true, 1>), gd, bd, 0, s, *a);
+        } else {
+            hipLaunchKernelGGL((k_fold<false, 1>), gd, bd, 0, s, *a);
+        }
+    } else if (nt) {
+        hipLaunchKernelGGL((k_fold<true, 2>), gd, bd, 0, s, *a);
     } else {
-        hipLaunchKernelGGL(k_fold<false>, dim3((unsigned)grid), dim3(kWavesPerBlock * 64), 0, s,
-                           *a);
+        hipLaunchKernelGGL((k_fold<false, 2>), gd, bd, 0, s, *a);
     }
     if (ev_stop) {
         (void)hipEventRecord((hipEvent_t)ev_stop, s);
