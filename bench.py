@@ -51,6 +51,8 @@ def _zipf(rank, world):
 
 
 CONFIGS = {
+    "1k_x_4KiB": ("1,000 msgs x 4 KiB (configs[0], the reference's CPU-only case; launch-bound "
+                  "on the GPU)", _uniform(1000, 4096), 0xB1A2E5, "weak"),
     "64k_x_64KiB": ("65,536 msgs x 64 KiB per GPU (configs[2], HBM-bound headline)",
                     _uniform(65536, 65536), 2, "weak"),
     "1M_x_256B": ("1,048,576 msgs x 256 B per GPU (configs[1], small-message regime)",
@@ -61,7 +63,8 @@ CONFIGS = {
                     _uniform(16, 256 << 20), 5, "weak"),
 }
 
-UNIFORM_SIZES = {"64k_x_64KiB": 65536, "1M_x_256B": 256, "16_x_256MiB": 256 << 20}
+UNIFORM_SIZES = {"1k_x_4KiB": 4096, "64k_x_64KiB": 65536, "1M_x_256B": 256,
+                 "16_x_256MiB": 256 << 20}
 
 
 def parse():
@@ -298,11 +301,15 @@ def main():
 
 
 def e2e(args, dev, stream, arena_dev, offs_np, lens_np, total_bytes, world, rank, dist, desc):
-    """End-to-end: payload starts in pinned host memory (broker blob buffers),
-    H2D copy + batch CRC + D2H of the CRCs, timed per step.  Reported in
-    DESIGN.md, never as the bench `value`."""
+    """End-to-end: the payload starts in host memory (broker blob buffers) and
+    the CRCs end there.  Two ways in, both timed per step (K steps after W):
+      staged    -- pinned host arena, H2D copy + batch CRC + D2H of the CRCs;
+      zero_copy -- ordinary host memory registered with bmqcrc_host_register,
+                   the kernels read it in place over PCIe, + D2H of the CRCs.
+    Reported in DESIGN.md, never as the bench `value`."""
+    import numpy as np
     import torch
-    from blazingmq_amd import Crc32c
+    from blazingmq_amd import Crc32c, HostRegistration, calculate_batch_ptr
     n = lens_np.size
     host = torch.empty(arena_dev.numel(), dtype=torch.uint8, pin_memory=True)
     host.copy_(arena_dev)
@@ -311,36 +318,58 @@ def e2e(args, dev, stream, arena_dev, offs_np, lens_np, total_bytes, world, rank
     out = torch.empty(n, dtype=torch.int32, device=dev)
     out_host = torch.empty(n, dtype=torch.int32, pin_memory=True)
 
-    def step():
+    def timed(step):
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize(dev)
+        return time.perf_counter() - t0
+
+    def staged():
         arena_dev.copy_(host, non_blocking=True)
         Crc32c.calculate_batch(arena_dev, offsets, lengths, None, out, seg_bytes=args.seg_bytes,
                                stream=stream, sync=False)
         out_host.copy_(out, non_blocking=True)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    el = time.perf_counter() - t0
-    # H2D alone
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        arena_dev.copy_(host, non_blocking=True)
-    torch.cuda.synchronize(dev)
-    h2d = time.perf_counter() - t0
+    el = timed(staged)
+    ref = out_host.numpy().copy()
+    h2d = timed(lambda: arena_dev.copy_(host, non_blocking=True))
+
+    pageable = np.empty(arena_dev.numel(), dtype=np.uint8)  # ordinary malloc'd host memory
+    pageable[:] = host.numpy()
+    with HostRegistration(pageable, device=dev.index) as reg:
+        def zero_copy():
+            calculate_batch_ptr(reg.dev_ptr, reg.nbytes, offsets, lengths, None, out,
+                                seg_bytes=args.seg_bytes, stream=stream, sync=False)
+            out_host.copy_(out, non_blocking=True)
+        el_zc = timed(zero_copy)
+    zc = out_host.numpy().copy()
+    resident = Crc32c.calculate_batch(arena_dev, offsets, lengths, seg_bytes=args.seg_bytes,
+                                      stream=stream).cpu().numpy()
+    same = bool(np.array_equal(zc, ref))
+    if not same:
+        bad = np.nonzero(zc != ref)[0]
+        print("e2e mismatch: %d of %d (first %s); staged vs resident %d, zero-copy vs resident %d"
+              % (bad.size, n, bad[:8].tolist(), int((ref != resident).sum()),
+                 int((zc != resident).sum())), file=sys.stderr, flush=True)
+    gib = total_bytes / 2**30 * args.steps
     if rank == 0:
         print(json.dumps({
-            "metric": "end-to-end CRC32C GiB/s incl. H2D payload + D2H CRCs (pinned host)",
-            "value": round(total_bytes * world / 2**30 * args.steps / el, 2), "unit": "GiB/s",
+            "metric": "end-to-end CRC32C GiB/s, payload in host memory, CRCs back to host",
+            "value": round(gib * world / el, 2), "unit": "GiB/s",
             "n_gpus": world, "steps": args.steps, "config": args.config + ": " + desc,
-            "h2d_only_GiBps": round(total_bytes / 2**30 * args.steps / h2d, 2),
-            "ms_per_step": round(1e3 * el / args.steps, 3)}), flush=True)
-    return 0
+            "staged_pinned_GiBps": round(gib / el, 2),
+            "h2d_only_GiBps": round(gib / h2d, 2),
+            "zero_copy_GiBps": round(gib / el_zc, 2),
+            "zero_copy_matches_staged": same,
+            "ms_per_step": round(1e3 * el / args.steps, 3),
+            "ms_per_step_zero_copy": round(1e3 * el_zc / args.steps, 3)}), flush=True)
+    return 0 if same else 1
 
 
 def _fill_slice(bmq, arena, seed, begin):

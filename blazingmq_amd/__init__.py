@@ -4,8 +4,9 @@ CRC32C integrity-checksum path (bmqp::Crc32c and its batch callers).
 The product is the C-ABI library ``lib/libbmqcrc.so`` (HIP kernels for gfx950
 + host dispatcher); this package is its Python host-side mirror.
 """
-from .crc32c import (Blob, BmqCrcError, Crc32c, calculate_batch_multi,  # noqa: F401
-                     device_count, fill_synthetic, kernel_timing, reserve)
+from .crc32c import (Blob, BmqCrcError, Crc32c, HostRegistration,  # noqa: F401
+                     calculate_batch_multi, calculate_batch_ptr, device_count, fill_synthetic,
+                     kernel_timing, reserve)
 
-__all__ = ["Blob", "BmqCrcError", "Crc32c", "calculate_batch_multi", "device_count",
-           "fill_synthetic", "kernel_timing", "reserve"]
+__all__ = ["Blob", "BmqCrcError", "Crc32c", "HostRegistration", "calculate_batch_multi",
+           "calculate_batch_ptr", "device_count", "fill_synthetic", "kernel_timing", "reserve"]

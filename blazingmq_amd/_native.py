@@ -72,6 +72,10 @@ lib.bmqcrc_fill_synthetic.argtypes = [_vp, _u64, _u64, _u64, ctypes.POINTER(Opts
 lib.bmqcrc_kernel_timing.restype = _int
 lib.bmqcrc_kernel_timing.argtypes = [_int, _vp, ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(_u32)]
+lib.bmqcrc_host_register.restype = _int
+lib.bmqcrc_host_register.argtypes = [_vp, _u64, _int, ctypes.POINTER(_vp)]
+lib.bmqcrc_host_unregister.restype = _int
+lib.bmqcrc_host_unregister.argtypes = [_vp]
 lib.bmqcrc_device_count.restype = _int
 lib.bmqcrc_device_count.argtypes = []
 lib.bmqcrc_last_error.restype = ctypes.c_char_p

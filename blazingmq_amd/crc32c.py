@@ -283,5 +283,52 @@ def reserve(device, stream, n_msgs, arena_bytes, seg_bytes=0):
                                              seg_bytes))
 
 
+class HostRegistration:
+    """Zero-copy view of a host array for the GPU (bmqcrc_host_register):
+    ``dev_ptr`` is the device-side address of ``array``'s first byte.  The
+    array must stay alive (and unmoved) until ``close()``."""
+
+    def __init__(self, array, device=-1):
+        self.array = np.ascontiguousarray(array).view(np.uint8).reshape(-1)
+        self.nbytes = self.array.size
+        p = ctypes.c_void_p()
+        _native.check(_native.lib.bmqcrc_host_register(self.array.ctypes.data, self.nbytes,
+                                                       device, ctypes.byref(p)))
+        self.dev_ptr = p.value
+        self._open = True
+
+    def close(self):
+        if self._open:
+            self._open = False
+            _native.check(_native.lib.bmqcrc_host_unregister(self.array.ctypes.data))
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def calculate_batch_ptr(arena_ptr, arena_bytes, offsets, lengths, seeds=None, out=None, *,
+                        seg_bytes=0, stream=None, sync=True):
+    """Batch over a device-visible arena given by address (a device allocation
+    or a ``HostRegistration.dev_ptr``); offsets/lengths/seeds/out as in
+    ``Crc32c.calculate_batch``'s torch form."""
+    import torch
+    dev = offsets.device
+    n = offsets.numel()
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+    if stream is None:
+        stream = torch.cuda.current_stream(dev)
+    flags = _native.BMQCRC_F_DEVICE_PTRS | (0 if sync else _native.BMQCRC_F_ASYNC)
+    o = _native.make_opts(device=dev.index if dev.index is not None else -1,
+                          stream=stream.cuda_stream, flags=flags, seg_bytes=seg_bytes)
+    _native.check(_native.lib.bmqcrc_crc32c_batch(
+        arena_ptr, arena_bytes, offsets.data_ptr(), lengths.data_ptr(),
+        seeds.data_ptr() if seeds is not None else None, out.data_ptr(), n, ctypes.byref(o)))
+    return out
+
+
 def device_count():
     return _native.lib.bmqcrc_device_count()

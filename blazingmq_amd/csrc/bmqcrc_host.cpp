@@ -109,7 +109,6 @@ struct Workspace {
 
 struct DeviceState {
     int num_cus = 0;
-    hipStream_t own_stream = nullptr;
 };
 
 std::mutex g_mu;
@@ -153,8 +152,6 @@ int device_state(int dev, DeviceState** st)
                                            ", this library is built for gfx950 (MI355X) only");
         }
         s.num_cus = prop.multiProcessorCount;
-        HIP_TRY(hipSetDevice(dev));
-        HIP_TRY(hipStreamCreateWithFlags(&s.own_stream, hipStreamNonBlocking));
     }
     *st = &s;
     return 0;
@@ -258,31 +255,35 @@ int open_ctx(int dev, void* user_stream, Ctx* c)
     }
     HIP_TRY(hipSetDevice(dev));
     c->dev = dev;
-    c->s = user_stream ? (hipStream_t)user_stream : c->st->own_stream;
+    c->s = (hipStream_t)user_stream;  // NULL: the device's default (null) stream, as in HIP
     c->w = workspace(dev, user_stream);
     return 0;
 }
 
 // Enqueue planner + fold on device pointers (caller holds c.w->mu).
 // Segment size (when the caller left it at 0) and k_fold blocks per CU, from
-// the batch's average message size.  Measured on MI355X:
-// batches of large messages stream fastest with long segments and one 4-wave
-// block per CU (64k x 64 KiB: 620 vs 646 us); small or mixed batches need
-// 16 KiB segments and two blocks per CU to hide latency (1M x 256 B: 60 vs
-// 81 us, Zipf: 4.35 vs 4.73 ms).  Segments stay short enough to leave at
-// least 1024 full groups of 64, one per wave of a 1-block-per-CU grid.
-void auto_shape(uint64_t n, uint64_t arena_bytes, uint32_t* seg, uint32_t* blocks_per_cu)
+// the batch's average message size and total bytes.  Measured on MI355X
+// (DESIGN.md section 6): batches of large messages stream fastest with long
+// segments and one 4-wave block per CU (64k x 64 KiB: 620 vs 646 us); small
+// or mixed batches need two blocks per CU to hide latency (1M x 256 B: 60 vs
+// 81 us, Zipf: 4.35 vs 4.73 ms).  The segment is the longest power of two
+// (64 KiB for large messages, 16 KiB otherwise, at least 256 B) that still
+// gives every wave slot of the grid a full group of 64 segments: a small
+// batch cut into few long segments would leave most CUs idle and run at the
+// latency of one lane's serial stream (1k x 4 KiB: 36 us in 16 KiB segments).
+void auto_shape(uint64_t n, uint64_t arena_bytes, int num_cus, uint32_t* seg,
+                uint32_t* blocks_per_cu)
 {
     const bool large = n > 0 && arena_bytes / n >= kDefaultSegBytes;
     *blocks_per_cu = large ? 1u : 2u;
     if (*seg == 0) {
-        *seg = kDefaultSegBytes;
-        for (uint32_t s = 4 * kDefaultSegBytes; large && s > kDefaultSegBytes; s >>= 1) {
-            if (arena_bytes / s >= 1024ull * kWaveLanes) {
-                *seg = s;
-                break;
-            }
+        const uint64_t slots = (uint64_t)(num_cus > 0 ? num_cus : 256) * *blocks_per_cu *
+                               kWavesPerBlock * kWaveLanes;
+        uint32_t s = large ? 4 * kDefaultSegBytes : kDefaultSegBytes;
+        while (s > 256 && arena_bytes / s < slots) {
+            s >>= 1;
         }
+        *seg = s;
     }
 }
 
@@ -294,7 +295,7 @@ int run_batch(Ctx& c, uint32_t flags, uint32_t seg, const void* arena, uint64_t 
     BatchArgs a;
     memset(&a, 0, sizeof(a));
     a.n = n;
-    auto_shape(n, arena_bytes, &seg, &a.blocks_per_cu);
+    auto_shape(n, arena_bytes, c.st->num_cus, &seg, &a.blocks_per_cu);
     a.seg_bytes = seg;
     static const uint32_t tune = [] {
         const char* e = getenv("BMQCRC_TUNE");  // experiment knob, see BatchArgs::tune
@@ -774,7 +775,7 @@ int bmqcrc_reserve(int device, void* stream, uint64_t n_msgs, uint64_t arena_byt
     std::lock_guard<std::mutex> g(w->mu);
     BatchArgs a;
     uint32_t per_cu;
-    auto_shape(n_msgs, arena_bytes, &seg_bytes, &per_cu);  // as the batch call will
+    auto_shape(n_msgs, arena_bytes, st->num_cus, &seg_bytes, &per_cu);  // as the batch call will
     return plan_ws(w, n_msgs, arena_bytes, seg_bytes, &a);
 }
 
@@ -794,7 +795,7 @@ int bmqcrc_fill_synthetic(void* dev_dst, uint64_t nbytes, uint64_t seed, uint64_
         return rc;
     }
     HIP_TRY(hipSetDevice(dev));
-    hipStream_t s = (opts && opts->stream) ? (hipStream_t)opts->stream : st->own_stream;
+    hipStream_t s = opts ? (hipStream_t)opts->stream : nullptr;
     if (bmqcrc_launch_fill((uint8_t*)dev_dst, nbytes, seed, begin, (void*)s)) {
         return fail(BMQCRC_EIO, "fill launch failed");
     }
@@ -831,6 +832,42 @@ int bmqcrc_kernel_timing(int device, void* stream, double* total_ms, uint32_t* c
     if (count) {
         *count = cnt;
     }
+    return 0;
+}
+
+int bmqcrc_host_register(void* host, uint64_t bytes, int device, void** dev_ptr)
+{
+    t_err.clear();
+    if (!host || !bytes || !dev_ptr) {
+        return fail(BMQCRC_EINVAL, "host, bytes and dev_ptr are required");
+    }
+    int dev, rc;
+    DeviceState* st = nullptr;
+    if ((rc = resolve_device(device, &dev)) || (rc = device_state(dev, &st))) {
+        return rc;
+    }
+    HIP_TRY(hipSetDevice(dev));
+    HIP_TRY(hipHostRegister(host, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
+    void* d = nullptr;
+    const hipError_t e = hipHostGetDevicePointer(&d, host, 0);
+    if (e != hipSuccess) {
+        (void)hipHostUnregister(host);
+        return fail(BMQCRC_EIO, std::string("hipHostGetDevicePointer: ") + hipGetErrorString(e));
+    }
+    *dev_ptr = d;
+    return 0;
+}
+
+int bmqcrc_host_unregister(void* host)
+{
+    t_err.clear();
+    if (!host) {
+        return fail(BMQCRC_EINVAL, "null host pointer");
+    }
+    if (device_count_raw() <= 0) {
+        return fail(BMQCRC_ENODEV, "no HIP device available");
+    }
+    HIP_TRY(hipHostUnregister(host));
     return 0;
 }
 

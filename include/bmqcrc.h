@@ -59,7 +59,7 @@ extern "C" {
 typedef struct bmqcrc_opts {
     uint32_t struct_size; /* sizeof(bmqcrc_opts) */
     int32_t device;       /* HIP device ordinal; -1 = current device */
-    void* stream;         /* hipStream_t; NULL = library-owned stream of that device */
+    void* stream;         /* hipStream_t; NULL = that device's default (null) stream */
     uint32_t flags;       /* BMQCRC_F_* */
     uint32_t seg_bytes;   /* segment size in bytes, multiple of 128 in [256, 2^30]; 0 = automatic:
                              16 KiB, or up to 64 KiB for batches of large messages */
@@ -135,6 +135,15 @@ int bmqcrc_fill_synthetic(void* dev_dst, uint64_t nbytes, uint64_t seed, uint64_
  * stream) recorded by calls with BMQCRC_F_TIME_KERNEL on (device, stream)
  * since the previous query; waits for those events, then resets. */
 int bmqcrc_kernel_timing(int device, void* stream, double* total_ms, uint32_t* count);
+
+/* Zero-copy input: page-lock `bytes` of ordinary host memory at `host` and map
+ * it into the GPU address space (hipHostRegister, mapped + portable).
+ * *dev_ptr receives the device-side address of `host`; pass it as the arena
+ * of a BMQCRC_F_DEVICE_PTRS batch and the kernels read the broker's blob
+ * buffers over PCIe in place, with no staging copy (SURVEY.md 8(d),
+ * end-to-end).  Undo with bmqcrc_host_unregister(host).  GPU only. */
+int bmqcrc_host_register(void* host, uint64_t bytes, int device, void** dev_ptr);
+int bmqcrc_host_unregister(void* host);
 
 /* Number of usable HIP devices (0 when none). */
 int bmqcrc_device_count(void);

@@ -29,7 +29,7 @@ def test_header_declares_expected_api():
               "bmqcrc_version", "bmqcrc_crc32c_verify", "bmqcrc_crc32c_blobs",
               "bmqcrc_put_event_scan", "bmqcrc_put_event_fill_crcs", "bmqcrc_put_event_verify",
               "bmqcrc_journal_scan", "bmqcrc_recover_verify", "bmqcrc_csl_scan",
-              "bmqcrc_csl_validate"):
+              "bmqcrc_csl_validate", "bmqcrc_host_register", "bmqcrc_host_unregister"):
         assert n in names
 
 

@@ -112,3 +112,16 @@ def test_batch_rejects_unknown_flags():
                                    out.ctypes.data, 1, ctypes.byref(o))
     if N.lib.bmqcrc_device_count() == 0:
         assert rc == N.BMQCRC_ENODEV
+
+
+def test_host_register_refuses_without_gpu():
+    import ctypes
+    import numpy as np
+    from blazingmq_amd import _native as N
+    a = np.zeros(4096, np.uint8)
+    p = ctypes.c_void_p()
+    assert N.lib.bmqcrc_host_register(None, 16, -1, ctypes.byref(p)) == N.BMQCRC_EINVAL
+    if N.lib.bmqcrc_device_count() == 0:
+        assert N.lib.bmqcrc_host_register(a.ctypes.data, a.size, -1,
+                                          ctypes.byref(p)) == N.BMQCRC_ENODEV
+        assert N.lib.bmqcrc_host_unregister(a.ctypes.data) == N.BMQCRC_ENODEV

@@ -115,3 +115,42 @@ def test_model_matches_oracle(seg):
     got = model_batch(arena, offs, lens, seeds, seg)
     exp = [oracle.crc32c(arena[o:o + l].tobytes(), s) for o, l, s in zip(offs, lens, seeds)]
     assert got == exp
+
+
+def _segment_pieces(arena, S, E, first, seed, lead_lines):
+    """The k_fold stream construction: lead_lines zero lines (right alignment
+    in the wave), then the segment's lines, where every 16-byte piece outside
+    [S, E) is a zero piece (the DMA reads the zero line) and only the pieces cut
+    by S or E are masked byte-exactly; the seed is XORed in last."""
+    L0 = S & ~127
+    need_end = max(E, S + 4) if first else E
+    nl = (need_end - L0 + 127) // 128
+    sl, el = S - L0, E - L0
+    gS, gE = sl // 16, (el + 15) // 16
+    line = bytearray(128 * nl)
+    for p in range(gS, gE):  # pieces read from HBM
+        line[16 * p:16 * p + 16] = arena[L0 + 16 * p:L0 + 16 * p + 16].tobytes()
+    if sl % 16:
+        line[16 * (sl // 16):sl] = bytes(sl - 16 * (sl // 16))
+    if el % 16:
+        line[el:16 * gE] = bytes(16 * gE - el)
+    if first:
+        for b in range(4):
+            line[sl + b] ^= ((~seed & 0xFFFFFFFF) >> (8 * b)) & 0xFF
+    return bytes(128 * lead_lines) + bytes(line), nl
+
+
+@pytest.mark.parametrize("lead", [0, 1, 5])
+def test_right_aligned_pieces_match_oracle(lead):
+    rng = np.random.default_rng(100 + lead)
+    arena = rng.integers(0, 256, size=8192, dtype=np.uint8)
+    for _ in range(60):
+        ln = int(rng.integers(0, 700))
+        off = int(rng.integers(0, arena.size - ln - 200))
+        seed = int(rng.integers(0, 2**32))
+        stream, nl = _segment_pieces(arena, off, off + ln, True, seed, lead)
+        words = [int(w) for w in np.frombuffer(stream, dtype="<u4")]
+        c = fold_stream(words)  # leading zero lines leave a zero-init CRC unchanged
+        padE = (off & ~127) + 128 * nl - (off + ln)
+        got = G.mulmod_r(c, xpow(-8 * padE)) ^ 0xFFFFFFFF
+        assert got == oracle.crc32c(arena[off:off + ln].tobytes(), seed), (off, ln, lead)

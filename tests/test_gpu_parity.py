@@ -327,3 +327,35 @@ def test_cpp_dropin_gpu_batch(cuda):
     env = dict(os.environ, BMQCRC_GOLDEN_DIR=os.path.join(os.path.dirname(__file__), "golden"))
     r = subprocess.run([exe, "gpu"], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0 and "PASS" in r.stdout, r.stdout + r.stderr
+
+
+def test_shape_hint_misprediction(cuda):
+    # After a closed-form batch (every message one segment) the next batch on
+    # the same stream skips the segment-map launches; a ragged batch then maps
+    # its segments by binary search in k_fold.  Both must be bit-exact, and so
+    # must the ragged batch after it (planned again) and a closed-form one after
+    # that (mispredicted the other way: map launches that exit early).
+    import torch
+    rng = np.random.default_rng(77)
+    arena_np = rng.integers(0, 256, size=6 << 20, dtype=np.uint8)
+    arena = torch.from_numpy(arena_np).to(cuda)
+    s = torch.cuda.Stream(cuda)
+
+    def run(lens):
+        lens = np.asarray(lens, np.uint32)
+        offs = np.array([rng.integers(0, arena_np.size - l + 1) for l in lens], np.int64)
+        seeds = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64).astype(np.uint32)
+        got = Crc32c.calculate_batch(arena, torch.from_numpy(offs).to(cuda),
+                                     torch.from_numpy(lens.view(np.int32)).to(cuda),
+                                     torch.from_numpy(seeds.view(np.int32)).to(cuda),
+                                     stream=s, seg_bytes=1024)
+        s.synchronize()
+        exp = oracle.batch(arena_np, offs, lens, seeds, nthreads=8)
+        bad = np.nonzero(got.cpu().numpy().view(np.uint32) != exp)[0]
+        assert bad.size == 0, [(int(i), int(lens[i])) for i in bad[:8]]
+
+    closed = rng.integers(1, 1025, size=5000)          # one segment each
+    uniform = np.full(3000, 3000)                       # three segments each
+    ragged = rng.integers(0, 20000, size=4000)
+    for lens in (closed, ragged, ragged, uniform, ragged, closed, closed):
+        run(lens)

@@ -92,3 +92,43 @@ def test_concurrent_streams_and_threads(cuda):
         exp = oracle.batch(arena_np, offs, lens, seeds, nthreads=8)
         for r in res:
             assert np.array_equal(r, exp)
+
+
+def test_zero_copy_host_arena(cuda):
+    # bmqcrc_host_register: the kernels read ordinary (registered) host memory
+    # in place over PCIe -- the zero-copy end-to-end variant of SURVEY.md 8(d)
+    import torch
+    from blazingmq_amd import HostRegistration, calculate_batch_ptr
+    rng = np.random.default_rng(51)
+    arena_np = rng.integers(0, 256, size=(2 << 20) + 77, dtype=np.uint8)
+    offs, lens, seeds = _batch(rng, 3000, 5000, arena_np.size)
+    with HostRegistration(arena_np, device=cuda.index or 0) as reg:
+        got = calculate_batch_ptr(reg.dev_ptr, reg.nbytes, torch.from_numpy(offs).to(cuda),
+                                  torch.from_numpy(lens.view(np.int32)).to(cuda),
+                                  torch.from_numpy(seeds.view(np.int32)).to(cuda))
+        got = got.cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, oracle.batch(arena_np, offs, lens, seeds, nthreads=8))
+
+
+def test_default_stream_ordering(cuda):
+    # opts.stream == NULL is the device's default (null) stream, so an ASYNC
+    # batch enqueued on torch's default stream is ordered with the torch ops
+    # that follow it there (here a non-blocking D2H copy, then a wait on that
+    # stream only) -- no device-wide synchronisation needed
+    import torch
+    from blazingmq_amd import fill_synthetic
+    rng = np.random.default_rng(61)
+    n, size = 50000, 1024
+    arena = torch.empty(n * size, dtype=torch.uint8, device=cuda)
+    fill_synthetic(arena, 9)
+    offs = np.arange(n, dtype=np.int64) * size
+    lens = np.full(n, size, np.uint32)
+    lens[rng.integers(0, n, 100)] = 0
+    with torch.cuda.stream(torch.cuda.default_stream(cuda)):
+        out = Crc32c.calculate_batch(arena, torch.from_numpy(offs).to(cuda),
+                                     torch.from_numpy(lens.view(np.int32)).to(cuda), sync=False)
+        host = torch.empty(n, dtype=torch.int32, pin_memory=True)
+        host.copy_(out, non_blocking=True)
+        torch.cuda.default_stream(cuda).synchronize()
+    exp = oracle.batch(arena.cpu().numpy(), offs, lens, nthreads=8)
+    assert np.array_equal(host.numpy().view(np.uint32), exp)
