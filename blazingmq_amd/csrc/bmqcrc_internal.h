@@ -19,17 +19,15 @@ constexpr int kPlanMaxBlocks = 256;  // planner grids stride over contiguous ran
 
 constexpr int kBuckets = 16;            // segment size classes: floor(log2(lines))
 
-// Control words written by the planner (device memory).
+// Control words of the segment-map launches (device memory).  The batch
+// totals (segment count, identity / uniform shape, block offsets) are not
+// stored: every consumer kernel derives them in its prologue from k_plan's
+// per-block words (block_sum), see plan_totals() in crc32c_kernels.hip.
 struct PlanCtrl {
-    uint32_t total_segs;   // number of segments in the batch
-    uint32_t identity;     // 1: every message is exactly one segment (segment g = message g)
     uint32_t sorted;       // 1: seginfo lists the segments grouped by size class
-    uint32_t ngroups;      // ceil(total_segs / 64)
-    uint32_t ticket_plan;  // last-block-done tickets (zeroed at allocation, reset by the
-    uint32_t ticket_hist;  //   last block of each launch)
-    uint32_t overflow;     // total_segs > max_segs: segment -> message by binary search
-    uint32_t nseg_uniform; // > 0: every message has exactly this many segments
-                           //     (segment g = message g / u, part g % u; no emit/sort)
+                           //    (written by k_plan_emit's last block, ragged batches only)
+    uint32_t ticket_hist;  // last-block-done ticket of k_plan_emit (zeroed at allocation,
+                           //    reset by the last block)
 };
 
 struct BatchArgs {
@@ -39,7 +37,9 @@ struct BatchArgs {
     const uint32_t* seeds;     // device, n, or nullptr (all zero)
     uint32_t* out;             // device, n
     uint32_t* seg_first;       // workspace, n: block-local exclusive prefix of segment counts
-    uint32_t* block_sum;       // workspace, 3 * nblocks: [sums | non-1 counts | block offsets]
+    uint32_t* block_sum;       // workspace, 3 * nblocks, per k_plan block: [segments |
+                               // messages with != 1 segment | segments per message if equal
+                               // for all the block's messages, else ~0]
     uint32_t* segmap;          // workspace, 2 * max_segs: (message, k) per segment, natural order
     uint32_t* seginfo;         // workspace, 2 * max_segs: (message, k) in size-class order
     uint32_t* bhist;           // workspace, kBuckets * nblocks_seg: histogram, then offsets

@@ -341,25 +341,97 @@ __device__ __forceinline__ void dma_round(uint32_t lds_dst, const uint64_t (&pba
         : "memory", "scc");
 }
 
-// Global exclusive prefix of segment counts: block-local part + block offset.
-__device__ __forceinline__ uint32_t seg_first_g(const BatchArgs& a, uint64_t i)
+// Global exclusive prefix of segment counts: block-local part + the k_plan
+// block's offset (boff: LDS, from plan_totals).
+__device__ __forceinline__ uint32_t seg_first_g(const BatchArgs& a, const uint32_t* boff,
+                                                uint64_t i)
 {
-    return a.seg_first[i] + a.block_sum[2u * a.nblocks + (uint32_t)(i / a.per_msg)];
+    return a.seg_first[i] + boff[(uint32_t)(i / a.per_msg)];
 }
 
 // Binary search: last message i with seg_first(i) <= g.
-__device__ uint32_t find_msg(const BatchArgs& a, uint32_t g)
+__device__ uint32_t find_msg(const BatchArgs& a, const uint32_t* boff, uint32_t g)
 {
     uint64_t lo = 0, hi = a.n;  // invariant: first(lo) <= g < first(hi) (hi == n: inf)
     while (hi - lo > 1) {
         const uint64_t mid = (lo + hi) >> 1;
-        if (seg_first_g(a, mid) <= g) {
+        if (seg_first_g(a, boff, mid) <= g) {
             lo = mid;
         } else {
             hi = mid;
         }
     }
     return (uint32_t)lo;
+}
+
+// Block-wide exclusive scan of v over blockDim.x threads (a multiple of 64,
+// at most 1024); returns the block total.  wsum: 33 words of LDS.
+__device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* excl, uint32_t* wsum)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nw = blockDim.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+        if (lane >= o) {
+            x += y;
+        }
+    }
+    if (lane == 63) {
+        wsum[wave] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x < 16) {
+        uint32_t w = (int)threadIdx.x < nw ? wsum[threadIdx.x] : 0u, y = w;
+        for (int o = 1; o < 16; o <<= 1) {
+            const uint32_t z = (uint32_t)__shfl_up((int)y, o, 16);
+            if ((int)threadIdx.x >= o) {
+                y += z;
+            }
+        }
+        wsum[16 + threadIdx.x] = y - w;  // exclusive wave prefix
+        if (threadIdx.x == 15) {
+            wsum[32] = y;
+        }
+    }
+    __syncthreads();
+    *excl = x - v + wsum[16 + wave];
+    const uint32_t tot = wsum[32];
+    __syncthreads();
+    return tot;
+}
+
+// Batch totals from k_plan's per-block words, derived by every block of a
+// consumer kernel in its prologue (blockDim.x >= nblocks): the segment count,
+// the identity / uniform shape, and the exclusive segment offset of every
+// k_plan block (-> boff in LDS).  Reading <= 3 x 256 L2-resident words per
+// block replaces a grid-wide arrival counter and a dependent last-block pass
+// at the end of k_plan.
+struct PlanTotals {
+    uint32_t total, identity, uni;
+};
+
+__device__ PlanTotals plan_totals(const BatchArgs& a, uint32_t* boff, uint32_t* wsum)
+{
+    const uint32_t j = threadIdx.x, nb = a.nblocks;
+    const uint32_t v = j < nb ? a.block_sum[j] : 0u;
+    const uint32_t nn = j < nb ? a.block_sum[nb + j] : 0u;
+    const uint32_t u0 = a.block_sum[2u * nb];
+    const uint32_t u = j < nb ? a.block_sum[2u * nb + j] : u0;
+    const int ragged = __syncthreads_or(nn != 0u);
+    const int mismatch = __syncthreads_or(u != u0);
+    uint32_t ex;
+    const uint32_t total = block_scan(v, &ex, wsum);
+    if (j < nb) {
+        boff[j] = ex;
+    }
+    __syncthreads();
+    PlanTotals t;
+    t.total = total;
+    t.identity = ragged ? 0u : 1u;  // every message exactly one segment
+    t.uni = (!mismatch && u0 != 0xffffffffu && u0 != 0u) ? u0 : 0u;
+    return t;
 }
 
 // Geometry of segment k of a message [mstart, mstart+len): byte range
@@ -394,8 +466,9 @@ struct SegDesc {
     uint32_t msg, k, len, seed;
 };
 
-__device__ __forceinline__ SegRef map_segment(const BatchArgs& a, uint32_t seg, bool valid,
-                                              uint32_t identity, uint32_t uni, uint32_t sorted)
+__device__ __forceinline__ SegRef map_segment(const BatchArgs& a, const uint32_t* boff,
+                                              uint32_t seg, bool valid, uint32_t identity,
+                                              uint32_t uni, uint32_t sorted)
 {
     SegRef r = {0u, 0u};
     if (valid) {
@@ -411,8 +484,8 @@ __device__ __forceinline__ SegRef map_segment(const BatchArgs& a, uint32_t seg, 
             r.msg = a.segmap[2u * seg];
             r.k = a.segmap[2u * seg + 1u];
         } else {
-            r.msg = find_msg(a, seg);  // no map (skipped or overflow): binary search
-            r.k = seg - seg_first_g(a, r.msg);
+            r.msg = find_msg(a, boff, seg);  // no map (skipped or overflow): binary search
+            r.k = seg - seg_first_g(a, boff, r.msg);
         }
     }
     return r;
@@ -449,12 +522,19 @@ __global__ __launch_bounds__(256, SLOTS == 1 ? 3 : 2) void k_fold(BatchArgs a)
     __syncthreads();
 
     // BMQCRC_F_WHOLE_MESSAGES: segment g = message g, one segment each, no
-    // planner ran (ctrl is not read)
+    // planner ran.  Otherwise the batch totals come from k_plan's block words.
+    __shared__ uint32_t boff[kPlanMaxBlocks];
+    __shared__ uint32_t wsum[40];
     const uint32_t whole = a.whole;
-    const uint32_t total = whole ? (uint32_t)a.n : a.ctrl->total_segs;
-    const uint32_t identity = whole ? 1u : a.ctrl->identity;
-    const uint32_t sorted = whole ? 0u : a.ctrl->sorted;
-    const uint32_t uni = whole ? 0u : a.ctrl->nseg_uniform;
+    PlanTotals pt = {(uint32_t)a.n, 1u, 0u};
+    if (!whole) {
+        pt = plan_totals(a, boff, wsum);
+    }
+    const uint32_t total = pt.total;
+    const uint32_t identity = pt.identity;
+    const uint32_t uni = pt.uni;
+    // the size-class order exists only if k_plan_emit/k_plan_scatter ran
+    const uint32_t sorted = (whole || !a.map_planned || identity || uni) ? 0u : a.ctrl->sorted;
     const uint32_t ngroups = (total + 63u) / 64u;
     const uint32_t SEG = a.seg_bytes;
     const uint64_t arena = (uint64_t)(uintptr_t)a.arena;
@@ -477,9 +557,11 @@ __global__ __launch_bounds__(256, SLOTS == 1 ? 3 : 2) void k_fold(BatchArgs a)
     SegRef ref2 = {0u, 0u};
     if (g < ngroups) {
         const uint32_t s0 = g * 64u + (uint32_t)lane;
-        nxt = fetch_desc(a, map_segment(a, s0, s0 < total, identity, uni, sorted), s0 < total);
+        nxt = fetch_desc(a, map_segment(a, boff, s0, s0 < total, identity, uni, sorted),
+                         s0 < total);
         const uint32_t s1 = (g + stride) * 64u + (uint32_t)lane;
-        ref2 = map_segment(a, s1, g + stride < ngroups && s1 < total, identity, uni, sorted);
+        ref2 = map_segment(a, boff, s1, g + stride < ngroups && s1 < total, identity, uni,
+                           sorted);
     }
     for (; g < ngroups; g += stride) {
         // ---------------------------------------------------- descriptor
@@ -491,8 +573,8 @@ __global__ __launch_bounds__(256, SLOTS == 1 ? 3 : 2) void k_fold(BatchArgs a)
             const bool v1 = g + stride < ngroups && s1 < total;
             nxt = fetch_desc(a, ref2, v1);
             const uint32_t s2 = (g + 2u * stride) * 64u + (uint32_t)lane;
-            ref2 = map_segment(a, s2, g + 2u * stride < ngroups && s2 < total, identity, uni,
-                               sorted);
+            ref2 = map_segment(a, boff, s2, g + 2u * stride < ngroups && s2 < total, identity,
+                               uni, sorted);
         }
         const uint32_t msg = cur.msg, k = cur.k, len = cur.len, seed = cur.seed;
         const uint64_t off = cur.off;
@@ -664,47 +746,14 @@ __device__ __forceinline__ bool last_block_arrival(uint32_t* ticket, uint32_t nb
     return *flag_lds != 0;
 }
 
-// Block-wide exclusive scan of v (1024 threads); returns the block total.
-__device__ __forceinline__ uint32_t block_scan_1024(uint32_t v, uint32_t* excl, uint32_t* wsum)
-{
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
-        if (lane >= o) {
-            x += y;
-        }
-    }
-    if (lane == 63) {
-        wsum[wave] = x;
-    }
-    __syncthreads();
-    if (threadIdx.x < 16) {
-        uint32_t w = wsum[threadIdx.x], y = w;
-        for (int o = 1; o < 16; o <<= 1) {
-            const uint32_t z = (uint32_t)__shfl_up((int)y, o, 16);
-            if ((int)threadIdx.x >= o) {
-                y += z;
-            }
-        }
-        wsum[16 + threadIdx.x] = y - w;  // exclusive wave prefix
-        if (threadIdx.x == 15) {
-            wsum[32] = y;
-        }
-    }
-    __syncthreads();
-    *excl = x - v + wsum[16 + wave];
-    const uint32_t tot = wsum[32];
-    __syncthreads();
-    return tot;
-}
-
-// K1: segment counts per message, block-local prefix over the block's
-// contiguous message range, and (last block) the prefix over blocks + totals.
-// Each thread takes kPlanV consecutive messages (a tile = 4096 messages, one
-// block scan) and the next tile's lengths are loaded before the current tile
-// is scanned, so a block pays one load latency, not one per tile.
+// K1: segment counts per message, the block-local exclusive prefix over the
+// block's contiguous message range (seg_first), out[] initialisation, and
+// three words per block (segments, messages with != 1 segment, the common
+// segment count or ~0) that the consumer kernels reduce in their prologues
+// (plan_totals).  No grid-wide step here.  Each thread takes kPlanV
+// consecutive messages (a tile = 4096 messages, one block scan) and the next
+// tile's lengths are loaded before the current tile is scanned, so a block
+// pays one load latency, not one per tile.
 constexpr uint32_t kPlanV = 4;
 __global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
 {
@@ -757,7 +806,7 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
             sum += ns[v];
         }
         uint32_t excl;
-        const uint32_t tot = block_scan_1024(sum, &excl, wsum);
+        const uint32_t tot = block_scan(sum, &excl, wsum);
         uint32_t run = carry + excl;
 #pragma unroll
         for (uint32_t v = 0; v < kPlanV; ++v) {
@@ -782,36 +831,10 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
         atomicAdd(&sh[1], non1);
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        publish(&a.block_sum[blockIdx.x], carry);
-        publish(&a.block_sum[a.nblocks + blockIdx.x], sh[1]);
-        publish(&a.block_sum[2u * a.nblocks + blockIdx.x], sh[2] == sh[3] ? sh[2] : 0xffffffffu);
-    }
-    if (!last_block_arrival(&a.ctrl->ticket_plan, a.nblocks, &sh[0])) {
-        return;
-    }
-    // last block (nblocks <= 1024): scan of the block totals, sc1 loads
-    const uint32_t j = threadIdx.x;
-    const uint32_t v = j < a.nblocks ? consume(&a.block_sum[j]) : 0u;
-    const uint32_t nn = j < a.nblocks ? consume(&a.block_sum[a.nblocks + j]) : 0u;
-    const uint32_t u0 = consume(&a.block_sum[2u * a.nblocks]);
-    const uint32_t u = j < a.nblocks ? consume(&a.block_sum[2u * a.nblocks + j]) : u0;
-    const int mismatch = __syncthreads_or(u != u0);
-    uint32_t ex;
-    const uint32_t total = block_scan_1024(v, &ex, wsum);
-    uint32_t ex2;
-    const uint32_t non1_all = block_scan_1024(nn, &ex2, wsum);
-    if (j < a.nblocks) {
-        a.block_sum[2u * a.nblocks + j] = ex;  // block offsets (read by later launches)
-    }
-    if (threadIdx.x == 0) {
-        a.ctrl->total_segs = total;
-        a.ctrl->identity = (non1_all == 0) ? 1u : 0u;
-        a.ctrl->ngroups = (total + 63u) / 64u;
-        a.ctrl->overflow = (total > a.max_segs) ? 1u : 0u;
-        a.ctrl->nseg_uniform = (!mismatch && u0 != 0xffffffffu && u0 != 0u) ? u0 : 0u;
-        a.ctrl->sorted = 0;
-        a.ctrl->ticket_plan = 0;  // for the next launch
+    if (threadIdx.x == 0) {  // read by the next launches (kernel boundary: plain stores)
+        a.block_sum[blockIdx.x] = carry;
+        a.block_sum[a.nblocks + blockIdx.x] = sh[1];
+        a.block_sum[2u * a.nblocks + blockIdx.x] = sh[2] == sh[3] ? sh[2] : 0xffffffffu;
     }
 }
 
@@ -842,11 +865,15 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_emit(BatchArgs a)
 {
     __shared__ uint32_t hist[kBuckets];
     __shared__ uint32_t flag;
-    if (a.ctrl->identity || a.ctrl->nseg_uniform) {
+    __shared__ uint32_t boff[kPlanMaxBlocks];
+    __shared__ uint32_t wsum[40];
+    const PlanTotals pt = plan_totals(a, boff, wsum);
+    if (pt.identity || pt.uni) {
         return;  // closed-form mapping; uniform across the grid: nobody takes a ticket
     }
-    const uint64_t total = a.ctrl->total_segs;
-    const uint64_t lim = total < a.max_segs ? total : a.max_segs;
+    const uint64_t total = pt.total;
+    const bool overflow = total > a.max_segs;
+    const uint64_t lim = overflow ? a.max_segs : total;
     if (threadIdx.x < kBuckets) {
         hist[threadIdx.x] = 0;
     }
@@ -860,14 +887,16 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_emit(BatchArgs a)
     const uint64_t lo = (uint64_t)blockIdx.x * a.per_seg;
     const uint64_t hi = min(lo + a.per_seg, lim);
     if (threadIdx.x == 0 && lo < hi) {
-        win_lo = find_msg(a, (uint32_t)lo);  // later tiles start where the last one ended
+        win_lo = find_msg(a, boff, (uint32_t)lo);  // later tiles start where the last one ended
     }
     __syncthreads();
     for (uint64_t base = lo; base < hi; base += kPlanBlock) {
         const uint64_t m0 = win_lo;
-        win[threadIdx.x] = (m0 + threadIdx.x < a.n) ? seg_first_g(a, m0 + threadIdx.x) : 0xffffffffu;
+        win[threadIdx.x] =
+            (m0 + threadIdx.x < a.n) ? seg_first_g(a, boff, m0 + threadIdx.x) : 0xffffffffu;
         if (threadIdx.x == 0) {
-            win[kPlanBlock] = (m0 + kPlanBlock < a.n) ? seg_first_g(a, m0 + kPlanBlock) : 0xffffffffu;
+            win[kPlanBlock] =
+                (m0 + kPlanBlock < a.n) ? seg_first_g(a, boff, m0 + kPlanBlock) : 0xffffffffu;
         }
         __syncthreads();
         const uint64_t g = base + threadIdx.x;
@@ -885,9 +914,9 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_emit(BatchArgs a)
                 }
                 msg = (uint32_t)m0 + l;
             } else {
-                msg = find_msg(a, (uint32_t)g);  // window exhausted (empty messages)
+                msg = find_msg(a, boff, (uint32_t)g);  // window exhausted (empty messages)
             }
-            const uint32_t k = (uint32_t)g - seg_first_g(a, msg);
+            const uint32_t k = (uint32_t)g - seg_first_g(a, boff, msg);
             a.segmap[2u * g] = msg;
             a.segmap[2u * g + 1u] = k;
             atomicAdd(&hist[seg_class(a, msg, k)], 1u);
@@ -942,7 +971,7 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_emit(BatchArgs a)
             acc += btot[c];
             used += btot[c] ? 1u : 0u;
         }
-        a.ctrl->sorted = (used > 1 && !a.ctrl->overflow) ? 1u : 0u;
+        a.ctrl->sorted = (used > 1 && !overflow) ? 1u : 0u;
         a.ctrl->ticket_hist = 0;
     }
     __syncthreads();
@@ -959,10 +988,13 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_scatter(BatchArgs a)
 {
     __shared__ uint32_t wcnt[16][kBuckets];
     __shared__ uint32_t run[kBuckets];
-    if (a.ctrl->identity || a.ctrl->nseg_uniform || !a.ctrl->sorted) {
+    __shared__ uint32_t boff[kPlanMaxBlocks];
+    __shared__ uint32_t wsum[40];
+    const PlanTotals pt = plan_totals(a, boff, wsum);
+    if (pt.identity || pt.uni || !a.ctrl->sorted) {
         return;
     }
-    const uint64_t total = a.ctrl->total_segs;
+    const uint64_t total = pt.total;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (threadIdx.x < kBuckets) {
         run[threadIdx.x] = a.bhist[(uint64_t)blockIdx.x * kBuckets + threadIdx.x];
