@@ -80,7 +80,7 @@ struct DevBuf {
 // Planner + staging scratch for one (device, stream).
 struct Workspace {
     std::mutex mu;
-    DevBuf seg_first, block_sum, segmap, seginfo, bhist, ctrl;
+    DevBuf seg_first, block_sum, seginfo, bhist, ctrl;
     // host-pointer staging
     DevBuf arena, offsets, lengths, seeds, out;
     // verify / blobs
@@ -89,7 +89,7 @@ struct Workspace {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timing, spare;
     // Shape of the last batch planned on this workspace, written by k_fold
     // into host-mapped memory (kHint*): after a closed-form batch the next
-    // one skips the k_plan_emit/k_plan_scatter launches.  A wrong guess only
+    // one skips the k_plan_hist/k_plan_sort launches.  A wrong guess only
     // costs speed (k_fold then maps segments by binary search).
     uint32_t* hint_host = nullptr;
     uint32_t* hint_dev = nullptr;
@@ -189,11 +189,10 @@ int plan_ws(Workspace* w, uint64_t n, uint64_t arena_bytes, uint32_t seg, BatchA
 {
     const uint64_t max_segs = max_segs_for(n, arena_bytes, seg);
     split_ranges(n, &a->per_msg, &a->nblocks);
-    split_ranges(max_segs, &a->per_seg, &a->nblocks_seg);
     int rc;
     if ((rc = w->seg_first.ensure(4 * std::max<uint64_t>(n, 1))) ||
         (rc = w->block_sum.ensure(12ull * kPlanMaxBlocks)) ||
-        (rc = w->segmap.ensure(8 * max_segs)) || (rc = w->seginfo.ensure(8 * max_segs)) ||
+        (rc = w->seginfo.ensure(8 * max_segs)) ||
         (rc = w->bhist.ensure(4ull * kBuckets * kPlanMaxBlocks)) ||
         (rc = w->ctrl.ensure(sizeof(PlanCtrl)))) {
         return rc;
@@ -220,7 +219,6 @@ int plan_ws(Workspace* w, uint64_t n, uint64_t arena_bytes, uint32_t seg, BatchA
     a->map_planned = 1;
     a->seg_first = (uint32_t*)w->seg_first.p;
     a->block_sum = (uint32_t*)w->block_sum.p;
-    a->segmap = (uint32_t*)w->segmap.p;
     a->seginfo = (uint32_t*)w->seginfo.p;
     a->bhist = (uint32_t*)w->bhist.p;
     a->ctrl = (PlanCtrl*)w->ctrl.p;

@@ -15,7 +15,7 @@ constexpr int kLdsBytes = kWavesPerBlock * kSlots * kSlotBytes;  // 64 KiB per b
 constexpr int kTabBytes = 8 * 256 * 4;  // remainder-reduction slicing tables (LDS)
 constexpr uint32_t kDefaultSegBytes = 16384;
 constexpr int kPlanBlock = 1024;
-constexpr int kPlanMaxBlocks = 256;  // planner grids stride over contiguous ranges
+constexpr int kPlanMaxBlocks = 256;  // planner grids: contiguous message ranges
 
 constexpr int kBuckets = 16;            // segment size classes: floor(log2(lines))
 
@@ -25,8 +25,8 @@ constexpr int kBuckets = 16;            // segment size classes: floor(log2(line
 // per-block words (block_sum), see plan_totals() in crc32c_kernels.hip.
 struct PlanCtrl {
     uint32_t sorted;       // 1: seginfo lists the segments grouped by size class
-                           //    (written by k_plan_emit's last block, ragged batches only)
-    uint32_t ticket_hist;  // last-block-done ticket of k_plan_emit (zeroed at allocation,
+                           //    (written by k_plan_hist's last block, ragged batches only)
+    uint32_t ticket_hist;  // last-block-done ticket of k_plan_hist (zeroed at allocation,
                            //    reset by the last block)
 };
 
@@ -40,23 +40,20 @@ struct BatchArgs {
     uint32_t* block_sum;       // workspace, 3 * nblocks, per k_plan block: [segments |
                                // messages with != 1 segment | segments per message if equal
                                // for all the block's messages, else ~0]
-    uint32_t* segmap;          // workspace, 2 * max_segs: (message, k) per segment, natural order
     uint32_t* seginfo;         // workspace, 2 * max_segs: (message, k) in size-class order
-    uint32_t* bhist;           // workspace, kBuckets * nblocks_seg: histogram, then offsets
+    uint32_t* bhist;           // workspace, kBuckets * nblocks: histogram, then offsets
     PlanCtrl* ctrl;            // workspace
     uint64_t n;
     uint64_t max_segs;
-    uint64_t per_msg;          // messages per k_plan block (multiple of kPlanBlock)
-    uint64_t per_seg;          // segments per k_plan_emit/k_plan_scatter block (idem)
+    uint64_t per_msg;          // messages per planner block (multiple of kPlanBlock)
     uint32_t seg_bytes;
-    uint32_t nblocks;          // k_plan blocks (<= kPlanMaxBlocks)
-    uint32_t nblocks_seg;      // k_plan_emit / k_plan_scatter blocks (<= kPlanMaxBlocks)
+    uint32_t nblocks;          // planner blocks (<= kPlanMaxBlocks)
     uint32_t whole;            // 1: BMQCRC_F_WHOLE_MESSAGES (one segment per message, no planner)
     uint32_t blocks_per_cu;    // k_fold grid: 1 (large messages) or 2 blocks per CU
     uint32_t tune;             // experiment knobs (BMQCRC_TUNE env): bit0 disables nt LDS-DMA
                                // loads, bit1 forces a 1-block/CU grid, bit3 forces 2, bit4
-                               // always launches k_plan_emit/k_plan_scatter
-    uint32_t map_planned;      // 1: k_plan_emit/k_plan_scatter run before k_fold; 0: they
+                               // always launches k_plan_hist/k_plan_sort
+    uint32_t map_planned;      // 1: k_plan_hist/k_plan_sort run before k_fold; 0: they
                                //    were skipped (the previous batch on this workspace was
                                //    closed-form) and a ragged batch maps segments by binary
                                //    search instead -- slower, never wrong

@@ -480,9 +480,6 @@ __device__ __forceinline__ SegRef map_segment(const BatchArgs& a, const uint32_t
         } else if (sorted) {
             r.msg = a.seginfo[2u * seg];
             r.k = a.seginfo[2u * seg + 1u];
-        } else if (a.map_planned && seg < a.max_segs) {
-            r.msg = a.segmap[2u * seg];
-            r.k = a.segmap[2u * seg + 1u];
         } else {
             r.msg = find_msg(a, boff, seg);  // no map (skipped or overflow): binary search
             r.k = seg - seg_first_g(a, boff, r.msg);
@@ -533,7 +530,7 @@ __global__ __launch_bounds__(256, SLOTS == 1 ? 3 : 2) void k_fold(BatchArgs a)
     const uint32_t total = pt.total;
     const uint32_t identity = pt.identity;
     const uint32_t uni = pt.uni;
-    // the size-class order exists only if k_plan_emit/k_plan_scatter ran
+    // the size-class order exists only if k_plan_hist/k_plan_sort ran
     const uint32_t sorted = (whole || !a.map_planned || identity || uni) ? 0u : a.ctrl->sorted;
     const uint32_t ngroups = (total + 63u) / 64u;
     const uint32_t SEG = a.seg_bytes;
@@ -849,19 +846,49 @@ __device__ __forceinline__ uint32_t size_class(uint32_t nl)
     return c < kBuckets - 1 ? c : kBuckets - 1;
 }
 
-// K2: segment -> message (binary search over the prefix), per-block size-class
-// histogram over the block's contiguous segment range, and (last block)
-// bucket-major offsets for the sort.
-__device__ __forceinline__ uint32_t seg_class(const BatchArgs& a, uint32_t msg, uint32_t k)
+// Segments of a message (offset off, length len) and the size class of its
+// last (or only) one.  Every other segment spans exactly seg_bytes / 128
+// lines (internal boundaries are 128-byte aligned and seg_bytes is a multiple
+// of 128), so it is in class size_class(seg_bytes / 128).
+__device__ __forceinline__ uint32_t msg_segments(const BatchArgs& a, uint64_t off, uint32_t len,
+                                                 uint32_t seg_shift, uint32_t* c_last)
 {
-    const uint32_t len = a.lengths[msg];
-    const uint32_t nseg = (len - 1u) / a.seg_bytes + 1u;
-    const SegGeom geo =
-        seg_geom((uint64_t)(uintptr_t)a.arena + a.offsets[msg], len, k, nseg, a.seg_bytes);
-    return size_class(geo.nl);
+    *c_last = kBuckets;  // kBuckets: no segment
+    if (len == 0) {
+        return 0;
+    }
+    const uint32_t SEG = a.seg_bytes;
+    const uint32_t nseg = (seg_shift ? ((len - 1u) >> seg_shift) : (len - 1u) / SEG) + 1u;
+    const SegGeom geo = seg_geom((uint64_t)(uintptr_t)a.arena + off, len, nseg - 1u, nseg, SEG);
+    *c_last = size_class(geo.nl);
+    return nseg;
 }
 
-__global__ __launch_bounds__(kPlanBlock) void k_plan_emit(BatchArgs a)
+// Lengths and offsets of a planner tile: kPlanV messages per thread, message
+// base + v * kPlanBlock + threadIdx.x (coalesced per v).  The next tile is
+// loaded while the current one is processed, so a block waits for one load
+// latency, not one per tile.
+struct TileDesc {
+    uint64_t off[kPlanV];
+    uint32_t len[kPlanV];
+};
+
+__device__ __forceinline__ void load_tile(const BatchArgs& a, uint64_t base, uint64_t hi,
+                                          TileDesc& t)
+{
+#pragma unroll
+    for (uint32_t v = 0; v < kPlanV; ++v) {
+        const uint64_t i = base + (uint64_t)v * kPlanBlock + threadIdx.x;
+        t.len[v] = i < hi ? a.lengths[i] : 0u;
+        t.off[v] = i < hi ? a.offsets[i] : 0ull;
+    }
+}
+
+// K2 (ragged batches): size-class histogram of each planner block's segments,
+// message-driven -- each thread takes whole messages, coalesced, so there is
+// no segment -> message search -- then (last block) bucket-major offsets over
+// (bucket, block) for the sort.
+__global__ __launch_bounds__(kPlanBlock) void k_plan_hist(BatchArgs a)
 {
     __shared__ uint32_t hist[kBuckets];
     __shared__ uint32_t flag;
@@ -871,60 +898,46 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_emit(BatchArgs a)
     if (pt.identity || pt.uni) {
         return;  // closed-form mapping; uniform across the grid: nobody takes a ticket
     }
-    const uint64_t total = pt.total;
-    const bool overflow = total > a.max_segs;
-    const uint64_t lim = overflow ? a.max_segs : total;
     if (threadIdx.x < kBuckets) {
         hist[threadIdx.x] = 0;
     }
     __syncthreads();
-    // Windowed search: the 1024 segments of a tile belong to a short run of
-    // consecutive messages, so one global binary search per tile (thread 0)
-    // plus a 1025-entry window of the prefix in LDS replaces a 22-step
-    // dependent global search per segment.
-    __shared__ uint32_t win[kPlanBlock + 1];
-    __shared__ uint32_t win_lo;
-    const uint64_t lo = (uint64_t)blockIdx.x * a.per_seg;
-    const uint64_t hi = min(lo + a.per_seg, lim);
-    if (threadIdx.x == 0 && lo < hi) {
-        win_lo = find_msg(a, boff, (uint32_t)lo);  // later tiles start where the last one ended
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t SEG = a.seg_bytes;
+    const uint32_t seg_shift = (SEG & (SEG - 1u)) == 0 ? (uint32_t)__builtin_ctz(SEG) : 0u;
+    const uint64_t lo = (uint64_t)blockIdx.x * a.per_msg;
+    const uint64_t hi = min(lo + a.per_msg, a.n);
+    uint32_t full = 0;  // this thread's non-last segments (all of class c_full)
+    constexpr uint64_t kTile = (uint64_t)kPlanBlock * kPlanV;
+    TileDesc nxt;
+    if (lo < hi) {
+        load_tile(a, lo, hi, nxt);
     }
-    __syncthreads();
-    for (uint64_t base = lo; base < hi; base += kPlanBlock) {
-        const uint64_t m0 = win_lo;
-        win[threadIdx.x] =
-            (m0 + threadIdx.x < a.n) ? seg_first_g(a, boff, m0 + threadIdx.x) : 0xffffffffu;
-        if (threadIdx.x == 0) {
-            win[kPlanBlock] =
-                (m0 + kPlanBlock < a.n) ? seg_first_g(a, boff, m0 + kPlanBlock) : 0xffffffffu;
+    for (uint64_t base = lo; base < hi; base += kTile) {
+        const TileDesc cur = nxt;
+        if (base + kTile < hi) {
+            load_tile(a, base + kTile, hi, nxt);
         }
-        __syncthreads();
-        const uint64_t g = base + threadIdx.x;
-        if (g < hi) {
-            uint32_t msg;
-            if ((uint32_t)g < win[kPlanBlock]) {
-                uint32_t l = 0, h = kPlanBlock;  // win[l] <= g < win[h]
-                while (h - l > 1) {
-                    const uint32_t mid = (l + h) >> 1;
-                    if (win[mid] <= (uint32_t)g) {
-                        l = mid;
-                    } else {
-                        h = mid;
-                    }
+#pragma unroll
+        for (uint32_t v = 0; v < kPlanV; ++v) {
+            uint32_t c;
+            const uint32_t nseg = msg_segments(a, cur.off[v], cur.len[v], seg_shift, &c);
+            full += nseg ? nseg - 1u : 0u;
+#pragma unroll
+            for (int cc = 0; cc < kBuckets; ++cc) {  // one LDS atomic per class in the wave
+                const uint64_t m = __ballot(c == (uint32_t)cc);
+                if (m && lane == 0) {
+                    atomicAdd(&hist[cc], (uint32_t)__popcll(m));
                 }
-                msg = (uint32_t)m0 + l;
-            } else {
-                msg = find_msg(a, boff, (uint32_t)g);  // window exhausted (empty messages)
-            }
-            const uint32_t k = (uint32_t)g - seg_first_g(a, boff, msg);
-            a.segmap[2u * g] = msg;
-            a.segmap[2u * g + 1u] = k;
-            atomicAdd(&hist[seg_class(a, msg, k)], 1u);
-            if (g + 1 == min(base + kPlanBlock, hi)) {
-                win_lo = msg;  // message of the tile's last segment starts the next window
             }
         }
-        __syncthreads();
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        full += (uint32_t)__shfl_xor((int)full, o);
+    }
+    if (lane == 0 && full) {
+        atomicAdd(&hist[size_class(SEG >> 7)], full);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -932,20 +945,18 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_emit(BatchArgs a)
             publish(&a.bhist[(uint64_t)blockIdx.x * kBuckets + c], hist[c]);
         }
     }
-    if (!last_block_arrival(&a.ctrl->ticket_hist, a.nblocks_seg, &flag)) {
+    if (!last_block_arrival(&a.ctrl->ticket_hist, a.nblocks, &flag)) {
         return;
     }
     // last block: bucket-major exclusive offsets over (bucket, block).  Wave c
     // scans bucket c over the blocks; thread 0 then scans the bucket totals.
     __shared__ uint32_t btot[kBuckets];
     __shared__ uint32_t bbase[kBuckets];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (wave < kBuckets) {
         uint32_t run = 0;
-        for (uint32_t base = 0; base < a.nblocks_seg; base += 64) {
+        for (uint32_t base = 0; base < a.nblocks; base += 64) {
             const uint32_t b = base + lane;
-            const uint32_t v =
-                b < a.nblocks_seg ? consume(&a.bhist[(uint64_t)b * kBuckets + wave]) : 0u;
+            const uint32_t v = b < a.nblocks ? consume(&a.bhist[(uint64_t)b * kBuckets + wave]) : 0u;
             uint32_t x = v;
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
@@ -954,7 +965,7 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_emit(BatchArgs a)
                     x += y;
                 }
             }
-            if (b < a.nblocks_seg) {
+            if (b < a.nblocks) {
                 a.bhist[(uint64_t)b * kBuckets + wave] = run + x - v;
             }
             run += (uint32_t)__shfl((int)x, 63);
@@ -965,28 +976,32 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_emit(BatchArgs a)
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint32_t acc = 0, used = 0;
+        uint32_t acc = 0;
         for (int c = 0; c < kBuckets; ++c) {
             bbase[c] = acc;
             acc += btot[c];
-            used += btot[c] ? 1u : 0u;
         }
-        a.ctrl->sorted = (used > 1 && !overflow) ? 1u : 0u;
+        // seginfo holds max_segs entries; past that k_fold searches instead
+        a.ctrl->sorted = (pt.total <= a.max_segs) ? 1u : 0u;
         a.ctrl->ticket_hist = 0;
     }
     __syncthreads();
     if (wave < kBuckets) {
-        for (uint32_t b = lane; b < a.nblocks_seg; b += 64) {
+        for (uint32_t b = lane; b < a.nblocks; b += 64) {
             a.bhist[(uint64_t)b * kBuckets + wave] += bbase[wave];
         }
     }
 }
 
-// K3: stable scatter of (message, k) into size-class order; each block walks
-// the same segment range in the same order as in K2.
-__global__ __launch_bounds__(kPlanBlock) void k_plan_scatter(BatchArgs a)
+// K3 (ragged batches): write (message, k) of every segment into seginfo in
+// size-class order.  Each block fills its slice of every bucket (offsets from
+// K2); a message's non-last segments go to one contiguous run (same class),
+// so they stay adjacent in a wave and combine before their one atomic.
+// Positions inside a block's slice are claimed with wave-aggregated LDS
+// atomics: the order within a bucket may differ between runs, the CRCs do not
+// (XOR combine).
+__global__ __launch_bounds__(kPlanBlock) void k_plan_sort(BatchArgs a)
 {
-    __shared__ uint32_t wcnt[16][kBuckets];
     __shared__ uint32_t run[kBuckets];
     __shared__ uint32_t boff[kPlanMaxBlocks];
     __shared__ uint32_t wsum[40];
@@ -994,52 +1009,88 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_scatter(BatchArgs a)
     if (pt.identity || pt.uni || !a.ctrl->sorted) {
         return;
     }
-    const uint64_t total = pt.total;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
     if (threadIdx.x < kBuckets) {
         run[threadIdx.x] = a.bhist[(uint64_t)blockIdx.x * kBuckets + threadIdx.x];
     }
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    const uint64_t lo = (uint64_t)blockIdx.x * a.per_seg;
-    const uint64_t hi = min(lo + a.per_seg, total);
-    for (uint64_t base = lo; base < hi; base += kPlanBlock) {
-        const uint64_t g = base + threadIdx.x;
-        uint32_t msg = 0, k = 0, cls = kBuckets;  // kBuckets: no segment
-        if (g < hi) {
-            msg = a.segmap[2u * g];
-            k = a.segmap[2u * g + 1u];
-            cls = seg_class(a, msg, k);
+    __syncthreads();
+    const uint32_t SEG = a.seg_bytes;
+    const uint32_t seg_shift = (SEG & (SEG - 1u)) == 0 ? (uint32_t)__builtin_ctz(SEG) : 0u;
+    const uint32_t c_full = size_class(SEG >> 7);
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint2* const info = (uint2*)a.seginfo;
+    const uint64_t lo = (uint64_t)blockIdx.x * a.per_msg;
+    const uint64_t hi = min(lo + a.per_msg, a.n);
+    constexpr uint64_t kTile = (uint64_t)kPlanBlock * kPlanV;
+    TileDesc nxt;
+    if (lo < hi) {
+        load_tile(a, lo, hi, nxt);
+    }
+    for (uint64_t base = lo; base < hi; base += kTile) {
+        const TileDesc cur = nxt;
+        if (base + kTile < hi) {
+            load_tile(a, base + kTile, hi, nxt);
         }
-        uint32_t rank = 0;
+        uint32_t c[kPlanV], nseg[kPlanV], nf_all = 0;
 #pragma unroll
-        for (int c = 0; c < kBuckets; ++c) {
-            const uint64_t m = __ballot(cls == (uint32_t)c);
-            if (cls == (uint32_t)c) {
-                rank = (uint32_t)__popcll(m & lt);
+        for (uint32_t v = 0; v < kPlanV; ++v) {
+            nseg[v] = msg_segments(a, cur.off[v], cur.len[v], seg_shift, &c[v]);
+            nf_all += nseg[v] ? nseg[v] - 1u : 0u;
+        }
+        // non-last segments: one contiguous run per message in class c_full,
+        // one LDS atomic per wave and tile
+        uint32_t x = nf_all;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+            if (lane >= o) {
+                x += y;
             }
+        }
+        const uint32_t tf = (uint32_t)__shfl((int)x, 63);
+        if (tf) {
+            uint32_t pos = 0;
             if (lane == 0) {
-                wcnt[wave][c] = (uint32_t)__popcll(m);
+                pos = atomicAdd(&run[c_full], tf);
+            }
+            pos = (uint32_t)__shfl((int)pos, 0) + (x - nf_all);
+#pragma unroll
+            for (uint32_t v = 0; v < kPlanV; ++v) {
+                const uint64_t i = base + (uint64_t)v * kPlanBlock + threadIdx.x;
+                const uint32_t nf = nseg[v] ? nseg[v] - 1u : 0u;
+                for (uint32_t k = 0; k < nf; ++k) {
+                    info[pos + k] = make_uint2((uint32_t)i, k);
+                }
+                pos += nf;
             }
         }
-        __syncthreads();
-        if (cls < kBuckets) {
-            uint32_t before = run[cls];
-            for (int w = 0; w < wave; ++w) {
-                before += wcnt[w][cls];
+        // last (or only) segments: per class, one LDS atomic per wave and tile
+#pragma unroll
+        for (int cc = 0; cc < kBuckets; ++cc) {
+            uint64_t m[kPlanV];
+            uint32_t tot = 0;
+#pragma unroll
+            for (uint32_t v = 0; v < kPlanV; ++v) {
+                m[v] = __ballot(c[v] == (uint32_t)cc);
+                tot += (uint32_t)__popcll(m[v]);
             }
-            const uint64_t pos = (uint64_t)before + rank;
-            a.seginfo[2u * pos] = msg;
-            a.seginfo[2u * pos + 1u] = k;
-        }
-        __syncthreads();
-        if (threadIdx.x < kBuckets) {
-            uint32_t t = 0;
-            for (int w = 0; w < 16; ++w) {
-                t += wcnt[w][threadIdx.x];
+            if (tot) {
+                uint32_t p = 0;
+                if (lane == 0) {
+                    p = atomicAdd(&run[cc], tot);
+                }
+                p = (uint32_t)__shfl((int)p, 0);
+#pragma unroll
+                for (uint32_t v = 0; v < kPlanV; ++v) {
+                    if (c[v] == (uint32_t)cc) {
+                        const uint64_t i = base + (uint64_t)v * kPlanBlock + threadIdx.x;
+                        info[p + (uint32_t)__popcll(m[v] & below)] =
+                            make_uint2((uint32_t)i, nseg[v] - 1u);
+                    }
+                    p += (uint32_t)__popcll(m[v]);
+                }
             }
-            run[threadIdx.x] += t;
         }
-        __syncthreads();
     }
 }
 
@@ -1191,8 +1242,8 @@ extern "C" int bmqcrc_launch_batch(const BatchArgs* a, void* stream, int num_cus
     if (!a->whole) {
         hipLaunchKernelGGL(k_plan, dim3(a->nblocks), dim3(kPlanBlock), 0, s, *a);
         if (a->map_planned) {
-            hipLaunchKernelGGL(k_plan_emit, dim3(a->nblocks_seg), dim3(kPlanBlock), 0, s, *a);
-            hipLaunchKernelGGL(k_plan_scatter, dim3(a->nblocks_seg), dim3(kPlanBlock), 0, s, *a);
+            hipLaunchKernelGGL(k_plan_hist, dim3(a->nblocks), dim3(kPlanBlock), 0, s, *a);
+            hipLaunchKernelGGL(k_plan_sort, dim3(a->nblocks), dim3(kPlanBlock), 0, s, *a);
         }
     }
     // tune bit5: one LDS slot per wave, three blocks per CU (3 waves per SIMD)
