@@ -341,21 +341,34 @@ __device__ __forceinline__ void dma_round(uint32_t lds_dst, const uint64_t (&pba
         : "memory", "scc");
 }
 
-// Global exclusive prefix of segment counts: block-local part + the k_plan
-// block's offset (boff: LDS, from plan_totals).
-__device__ __forceinline__ uint32_t seg_first_g(const BatchArgs& a, const uint32_t* boff,
-                                                uint64_t i)
+// Planner words every consumer block keeps in LDS (filled by plan_totals):
+// the exclusive segment offset of each k_plan block and its common segment
+// count per message (~0 when its messages differ).
+struct PlanLds {
+    uint32_t boff[kPlanMaxBlocks];
+    uint32_t bu[kPlanMaxBlocks];
+    uint32_t wsum[40];
+};
+
+// Global exclusive prefix of segment counts: the k_plan block's offset plus,
+// within the block, i's rank times the common count when the block is
+// uniform (k_plan then skips seg_first for single-tile blocks), else the
+// block-local prefix k_plan stored.
+__device__ __forceinline__ uint32_t seg_first_g(const BatchArgs& a, const PlanLds* pl, uint64_t i)
 {
-    return a.seg_first[i] + boff[(uint32_t)(i / a.per_msg)];
+    const uint32_t b = (uint32_t)(i / a.per_msg);
+    const uint32_t u = pl->bu[b];
+    return pl->boff[b] +
+           (u != 0xffffffffu ? (uint32_t)(i - (uint64_t)b * a.per_msg) * u : a.seg_first[i]);
 }
 
 // Binary search: last message i with seg_first(i) <= g.
-__device__ uint32_t find_msg(const BatchArgs& a, const uint32_t* boff, uint32_t g)
+__device__ uint32_t find_msg(const BatchArgs& a, const PlanLds* pl, uint32_t g)
 {
     uint64_t lo = 0, hi = a.n;  // invariant: first(lo) <= g < first(hi) (hi == n: inf)
     while (hi - lo > 1) {
         const uint64_t mid = (lo + hi) >> 1;
-        if (seg_first_g(a, boff, mid) <= g) {
+        if (seg_first_g(a, pl, mid) <= g) {
             lo = mid;
         } else {
             hi = mid;
@@ -412,7 +425,7 @@ struct PlanTotals {
     uint32_t total, identity, uni;
 };
 
-__device__ PlanTotals plan_totals(const BatchArgs& a, uint32_t* boff, uint32_t* wsum)
+__device__ PlanTotals plan_totals(const BatchArgs& a, PlanLds* pl)
 {
     const uint32_t j = threadIdx.x, nb = a.nblocks;
     const uint32_t v = j < nb ? a.block_sum[j] : 0u;
@@ -422,9 +435,10 @@ __device__ PlanTotals plan_totals(const BatchArgs& a, uint32_t* boff, uint32_t* 
     const int ragged = __syncthreads_or(nn != 0u);
     const int mismatch = __syncthreads_or(u != u0);
     uint32_t ex;
-    const uint32_t total = block_scan(v, &ex, wsum);
+    const uint32_t total = block_scan(v, &ex, pl->wsum);
     if (j < nb) {
-        boff[j] = ex;
+        pl->boff[j] = ex;
+        pl->bu[j] = u;
     }
     __syncthreads();
     PlanTotals t;
@@ -466,7 +480,7 @@ struct SegDesc {
     uint32_t msg, k, len, seed;
 };
 
-__device__ __forceinline__ SegRef map_segment(const BatchArgs& a, const uint32_t* boff,
+__device__ __forceinline__ SegRef map_segment(const BatchArgs& a, const PlanLds* pl,
                                               uint32_t seg, bool valid, uint32_t identity,
                                               uint32_t uni, uint32_t sorted)
 {
@@ -481,8 +495,8 @@ __device__ __forceinline__ SegRef map_segment(const BatchArgs& a, const uint32_t
             r.msg = a.seginfo[2u * seg];
             r.k = a.seginfo[2u * seg + 1u];
         } else {
-            r.msg = find_msg(a, boff, seg);  // no map (skipped or overflow): binary search
-            r.k = seg - seg_first_g(a, boff, r.msg);
+            r.msg = find_msg(a, pl, seg);  // no map (skipped or overflow): binary search
+            r.k = seg - seg_first_g(a, pl, r.msg);
         }
     }
     return r;
@@ -520,12 +534,11 @@ __global__ __launch_bounds__(256, SLOTS == 1 ? 3 : 2) void k_fold(BatchArgs a)
 
     // BMQCRC_F_WHOLE_MESSAGES: segment g = message g, one segment each, no
     // planner ran.  Otherwise the batch totals come from k_plan's block words.
-    __shared__ uint32_t boff[kPlanMaxBlocks];
-    __shared__ uint32_t wsum[40];
+    __shared__ PlanLds pl;
     const uint32_t whole = a.whole;
     PlanTotals pt = {(uint32_t)a.n, 1u, 0u};
     if (!whole) {
-        pt = plan_totals(a, boff, wsum);
+        pt = plan_totals(a, &pl);
     }
     const uint32_t total = pt.total;
     const uint32_t identity = pt.identity;
@@ -554,10 +567,10 @@ __global__ __launch_bounds__(256, SLOTS == 1 ? 3 : 2) void k_fold(BatchArgs a)
     SegRef ref2 = {0u, 0u};
     if (g < ngroups) {
         const uint32_t s0 = g * 64u + (uint32_t)lane;
-        nxt = fetch_desc(a, map_segment(a, boff, s0, s0 < total, identity, uni, sorted),
+        nxt = fetch_desc(a, map_segment(a, &pl, s0, s0 < total, identity, uni, sorted),
                          s0 < total);
         const uint32_t s1 = (g + stride) * 64u + (uint32_t)lane;
-        ref2 = map_segment(a, boff, s1, g + stride < ngroups && s1 < total, identity, uni,
+        ref2 = map_segment(a, &pl, s1, g + stride < ngroups && s1 < total, identity, uni,
                            sorted);
     }
     for (; g < ngroups; g += stride) {
@@ -570,7 +583,7 @@ __global__ __launch_bounds__(256, SLOTS == 1 ? 3 : 2) void k_fold(BatchArgs a)
             const bool v1 = g + stride < ngroups && s1 < total;
             nxt = fetch_desc(a, ref2, v1);
             const uint32_t s2 = (g + 2u * stride) * 64u + (uint32_t)lane;
-            ref2 = map_segment(a, boff, s2, g + 2u * stride < ngroups && s2 < total, identity,
+            ref2 = map_segment(a, &pl, s2, g + 2u * stride < ngroups && s2 < total, identity,
                                uni, sorted);
         }
         const uint32_t msg = cur.msg, k = cur.k, len = cur.len, seed = cur.seed;
@@ -778,7 +791,12 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
     if (lo < hi) {
         load(lo, nxt);
     }
+    // A single-tile block (<= 4096 messages: every batch of <= 1M messages)
+    // writes seg_first only if its messages differ in segment count; for a
+    // uniform block consumers compute it (seg_first_g).
+    const bool one_tile = hi - lo <= kTile;
     uint32_t carry = 0, mn = 0xffffffffu, mx = 0, non1 = 0;
+    uint32_t ns[kPlanV], run0 = 0;
     for (uint64_t base = lo; base < hi; base += kTile) {
         uint32_t L[kPlanV];
 #pragma unroll
@@ -788,14 +806,18 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
         if (base + kTile < hi) {
             load(base + kTile, nxt);  // next tile in flight during this scan
         }
-        uint32_t ns[kPlanV], sum = 0;
+        uint32_t sum = 0;
 #pragma unroll
         for (uint32_t v = 0; v < kPlanV; ++v) {
             const uint64_t i = base + (uint64_t)threadIdx.x * kPlanV + v;
             const uint32_t len = L[v];
             ns[v] = len ? (seg_shift ? ((len - 1u) >> seg_shift) : (len - 1u) / seg) + 1u : 0u;
             if (i < hi) {
-                a.out[i] = len ? 0u : (a.seeds ? a.seeds[i] : 0u);
+                // a one-segment message is stored whole by its lane in k_fold;
+                // others XOR-accumulate (from 0) or keep the seed (empty)
+                if (ns[v] != 1u) {
+                    a.out[i] = len ? 0u : (a.seeds ? a.seeds[i] : 0u);
+                }
                 mn = min(mn, ns[v]);
                 mx = max(mx, ns[v]);
                 non1 += ns[v] != 1u ? 1u : 0u;
@@ -804,14 +826,17 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
         }
         uint32_t excl;
         const uint32_t tot = block_scan(sum, &excl, wsum);
-        uint32_t run = carry + excl;
+        run0 = carry + excl;
+        if (!one_tile) {
+            uint32_t run = run0;
 #pragma unroll
-        for (uint32_t v = 0; v < kPlanV; ++v) {
-            const uint64_t i = base + (uint64_t)threadIdx.x * kPlanV + v;
-            if (i < hi) {
-                a.seg_first[i] = run;
+            for (uint32_t v = 0; v < kPlanV; ++v) {
+                const uint64_t i = base + (uint64_t)threadIdx.x * kPlanV + v;
+                if (i < hi) {
+                    a.seg_first[i] = run;
+                }
+                run += ns[v];
             }
-            run += ns[v];
         }
         carry += tot;
     }
@@ -828,6 +853,17 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
         atomicAdd(&sh[1], non1);
     }
     __syncthreads();
+    if (one_tile && sh[2] != sh[3]) {
+        uint32_t run = run0;
+#pragma unroll
+        for (uint32_t v = 0; v < kPlanV; ++v) {
+            const uint64_t i = lo + (uint64_t)threadIdx.x * kPlanV + v;
+            if (i < hi) {
+                a.seg_first[i] = run;
+            }
+            run += ns[v];
+        }
+    }
     if (threadIdx.x == 0) {  // read by the next launches (kernel boundary: plain stores)
         a.block_sum[blockIdx.x] = carry;
         a.block_sum[a.nblocks + blockIdx.x] = sh[1];
@@ -892,9 +928,8 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_hist(BatchArgs a)
 {
     __shared__ uint32_t hist[kBuckets];
     __shared__ uint32_t flag;
-    __shared__ uint32_t boff[kPlanMaxBlocks];
-    __shared__ uint32_t wsum[40];
-    const PlanTotals pt = plan_totals(a, boff, wsum);
+    __shared__ PlanLds pl;
+    const PlanTotals pt = plan_totals(a, &pl);
     if (pt.identity || pt.uni) {
         return;  // closed-form mapping; uniform across the grid: nobody takes a ticket
     }
@@ -1003,9 +1038,8 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_hist(BatchArgs a)
 __global__ __launch_bounds__(kPlanBlock) void k_plan_sort(BatchArgs a)
 {
     __shared__ uint32_t run[kBuckets];
-    __shared__ uint32_t boff[kPlanMaxBlocks];
-    __shared__ uint32_t wsum[40];
-    const PlanTotals pt = plan_totals(a, boff, wsum);
+    __shared__ PlanLds pl;
+    const PlanTotals pt = plan_totals(a, &pl);
     if (pt.identity || pt.uni || !a.ctrl->sorted) {
         return;
     }

@@ -357,5 +357,8 @@ def test_shape_hint_misprediction(cuda):
     closed = rng.integers(1, 1025, size=5000)          # one segment each
     uniform = np.full(3000, 3000)                       # three segments each
     ragged = rng.integers(0, 20000, size=4000)
-    for lens in (closed, ragged, ragged, uniform, ragged, closed, closed):
+    # planner blocks of 1024 messages: the first five uniform (k_plan skips
+    # their seg_first, the binary search recomputes it), the rest ragged
+    mixed = np.concatenate([rng.integers(1, 1025, size=5120), rng.integers(0, 9000, size=3000)])
+    for lens in (closed, mixed, closed, ragged, ragged, uniform, ragged, closed, mixed, closed):
         run(lens)
