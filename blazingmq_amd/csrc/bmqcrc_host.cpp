@@ -261,27 +261,42 @@ int open_ctx(int dev, void* user_stream, Ctx* c)
 // Enqueue planner + fold on device pointers (caller holds c.w->mu).
 // Segment size (when the caller left it at 0) and k_fold blocks per CU, from
 // the batch's average message size and total bytes.  Measured on MI355X
-// (DESIGN.md section 6): batches of large messages stream fastest with long
-// segments and one 4-wave block per CU (64k x 64 KiB: 620 vs 646 us); small
-// or mixed batches need two blocks per CU to hide latency (1M x 256 B: 60 vs
-// 81 us, Zipf: 4.35 vs 4.73 ms).  The segment is the longest power of two
-// (64 KiB for large messages, 16 KiB otherwise, at least 256 B) that still
-// gives every wave slot of the grid a full group of 64 segments: a small
-// batch cut into few long segments would leave most CUs idle and run at the
-// latency of one lane's serial stream (1k x 4 KiB: 36 us in 16 KiB segments).
+// (profiles/r01/sweeps/shape_sweep*.jsonl):
+//  * >= 4 GiB of >= 16 KiB messages: 64 KiB segments, one 4-wave block per CU
+//    (64k x 64 KiB: 620 us, the fastest shape);
+//  * otherwise two blocks per CU, and 16 KiB segments when that still gives
+//    every wave slot a group of 64 (Zipf 4M, 2 GiB of 64 KiB messages);
+//  * smaller batches: the longest of 2 KiB, 1 KiB, 512 B, 256 B that gives
+//    every wave two groups, so each wave streams steadily: 256 MiB of 64 KiB
+//    messages 72 -> 56 us, 1k x 4 KiB 36 -> 13 us.  4 and 8 KiB segments
+//    measured 10-30 % slower than both 2 and 16 KiB at every size tried.
 void auto_shape(uint64_t n, uint64_t arena_bytes, int num_cus, uint32_t* seg,
                 uint32_t* blocks_per_cu)
 {
+    const uint64_t cus = (uint64_t)(num_cus > 0 ? num_cus : 256);
+    const uint64_t wave_segs = (uint64_t)kWavesPerBlock * kWaveLanes;  // per block
     const bool large = n > 0 && arena_bytes / n >= kDefaultSegBytes;
-    *blocks_per_cu = large ? 1u : 2u;
-    if (*seg == 0) {
-        const uint64_t slots = (uint64_t)(num_cus > 0 ? num_cus : 256) * *blocks_per_cu *
-                               kWavesPerBlock * kWaveLanes;
-        uint32_t s = large ? 4 * kDefaultSegBytes : kDefaultSegBytes;
-        while (s > 256 && arena_bytes / s < slots) {
-            s >>= 1;
+    if (large && arena_bytes / (4 * kDefaultSegBytes) >= cus * wave_segs) {
+        *blocks_per_cu = 1;
+        if (*seg == 0) {
+            *seg = 4 * kDefaultSegBytes;
         }
-        *seg = s;
+        return;
+    }
+    *blocks_per_cu = 2;
+    if (*seg == 0) {
+        const uint64_t slots = cus * 2 * wave_segs;
+        if (arena_bytes / kDefaultSegBytes >= slots) {
+            *seg = kDefaultSegBytes;
+            return;
+        }
+        *seg = 256;
+        for (uint32_t s : {2048u, 1024u, 512u}) {
+            if (arena_bytes / s >= 2 * slots) {
+                *seg = s;
+                break;
+            }
+        }
     }
 }
 

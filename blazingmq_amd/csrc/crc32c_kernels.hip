@@ -23,7 +23,7 @@
 //     are read from a zero line instead, so only the 16-byte pieces cut by a
 //     segment's first or last byte need a byte mask (a few LDS
 //     read-modify-writes).  Two LDS slots per wave: round r+1 is in flight
-//     while round r folds (one slot in the 4-blocks-per-CU variant).
+//     while round r folds.
 //   * Streams are right-aligned in the wave: a lane with nl lines starts at
 //     round R - nl (R = the wave's longest stream) and folds zero lines
 //     before that, which leaves a zero-init CRC unchanged.  Every lane thus
@@ -513,18 +513,15 @@ __device__ __forceinline__ SegDesc fetch_desc(const BatchArgs& a, SegRef r, bool
     return d;
 }
 
-// SLOTS = LDS ring depth per wave: 2 (two 4-wave blocks per CU, or one for
-// large-message batches) or 1 (three blocks per CU: 40 KiB of LDS each).
-template <bool NT, int SLOTS>
-__global__ __launch_bounds__(256, SLOTS == 1 ? 3 : 2) void k_fold(BatchArgs a)
+template <bool NT>
+__global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
 {
-    __shared__ __attribute__((aligned(16)))
-    uint8_t lds[kTabBytes + kWavesPerBlock * SLOTS * kSlotBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kTabBytes + kLdsBytes];
 
     const int lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t tab_lds = (uint32_t)(uintptr_t)(lds_u8*)lds;
-    const uint32_t wave_lds = tab_lds + kTabBytes + wave * (SLOTS * kSlotBytes);
+    const uint32_t wave_lds = tab_lds + kTabBytes + wave * (kSlots * kSlotBytes);
 
     // remainder-reduction tables -> LDS (8 KiB, once per block; no DMA in flight yet)
     for (uint32_t t = threadIdx.x; t < 8u * 256u; t += blockDim.x) {
@@ -636,12 +633,12 @@ __global__ __launch_bounds__(256, SLOTS == 1 ? 3 : 2) void k_fold(BatchArgs a)
         const uint32_t c0 = ~seed;
 
         dma_round<NT>(wave_lds, pbase, plo, pcnt, zero, 0);
-        if (SLOTS == 2 && R > 1) {
+        if (R > 1) {
             dma_round<NT>(wave_lds + kSlotBytes, pbase, plo, pcnt, zero, 1);
         }
         for (uint32_t r = 0; r < R; ++r) {
-            const uint32_t slot = wave_lds + (SLOTS == 2 ? (r & 1u) * kSlotBytes : 0u);
-            if (SLOTS == 2 && r + 1 < R) {
+            const uint32_t slot = wave_lds + (r & 1u) * kSlotBytes;
+            if (r + 1 < R) {
                 asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
             } else {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -669,8 +666,8 @@ __global__ __launch_bounds__(256, SLOTS == 1 ? 3 : 2) void k_fold(BatchArgs a)
                 m[4 * kk + 2] = v.z;
                 m[4 * kk + 3] = v.w;
             }
-            if (r + SLOTS < R) {
-                dma_round<NT>(slot, pbase, plo, pcnt, zero, r + SLOTS);
+            if (r + 2 < R) {
+                dma_round<NT>(slot, pbase, plo, pcnt, zero, r + 2);
             }
             if (r + 1 < R) {
                 fold_round(q, m);
@@ -1280,12 +1277,9 @@ extern "C" int bmqcrc_launch_batch(const BatchArgs* a, void* stream, int num_cus
             hipLaunchKernelGGL(k_plan_sort, dim3(a->nblocks), dim3(kPlanBlock), 0, s, *a);
         }
     }
-    // tune bit5: one LDS slot per wave, three blocks per CU (3 waves per SIMD)
-    const bool one_slot = (a->tune & 32u) != 0;
     const uint64_t max_groups = (a->max_segs + 63) / 64;
     uint64_t grid = (max_groups + kWavesPerBlock - 1) / kWavesPerBlock;
-    const uint32_t per_cu =
-        one_slot ? 3u : (a->tune & 2u) ? 1u : (a->tune & 8u) ? 2u : a->blocks_per_cu;
+    const uint32_t per_cu = (a->tune & 2u) ? 1u : (a->tune & 8u) ? 2u : a->blocks_per_cu;
     const uint64_t cap = (uint64_t)(num_cus > 0 ? num_cus : 256) * (per_cu ? per_cu : 2u);
     if (grid > cap) {
         grid = cap;
@@ -1296,18 +1290,11 @@ extern "C" int bmqcrc_launch_batch(const BatchArgs* a, void* stream, int num_cus
     if (ev_start) {
         (void)hipEventRecord((hipEvent_t)ev_start, s);
     }
-    const dim3 gd((unsigned)grid), bd(kWavesPerBlock * 64);
-    const bool nt = !(a->tune & 1u);  // default: non-temporal LDS-DMA (once-read stream)
-    if (one_slot) {
-        if (nt) {
-            hipLaunchKernelGGL((k_fold<true, 1>), gd, bd, 0, s, *a);
-        } else {
-            hipLaunchKernelGGL((k_fold<false, 1>), gd, bd, 0, s, *a);
-        }
-    } else if (nt) {
-        hipLaunchKernelGGL((k_fold<true, 2>), gd, bd, 0, s, *a);
+    if (!(a->tune & 1u)) {  // default: non-temporal LDS-DMA (once-read stream)
+        hipLaunchKernelGGL(k_fold<true>, dim3((unsigned)grid), dim3(kWavesPerBlock * 64), 0, s, *a);
     } else {
-        hipLaunchKernelGGL((k_fold<false, 2>), gd, bd, 0, s, *a);
+        hipLaunchKernelGGL(k_fold<false>, dim3((unsigned)grid), dim3(kWavesPerBlock * 64), 0, s,
+                           *a);
     }
     if (ev_stop) {
         (void)hipEventRecord((hipEvent_t)ev_stop, s);

@@ -1,4 +1,6 @@
-# k_fold time and step rate vs message size at a fixed 256 MiB batch
+#!/usr/bin/env python3
+"""k_fold time and step rate vs message size at a fixed 256 MiB batch, planned
+and BMQCRC_F_WHOLE_MESSAGES, one JSON line per point (GPU box)."""
 import os, sys, json, time
 sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "/root/repo"))
 import numpy as np, torch
