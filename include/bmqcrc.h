@@ -61,8 +61,8 @@ typedef struct bmqcrc_opts {
     int32_t device;       /* HIP device ordinal; -1 = current device */
     void* stream;         /* hipStream_t; NULL = that device's default (null) stream */
     uint32_t flags;       /* BMQCRC_F_* */
-    uint32_t seg_bytes;   /* segment size in bytes, multiple of 128 in [256, 2^30]; 0 = automatic:
-                             16 KiB, or up to 64 KiB for batches of large messages */
+    uint32_t seg_bytes;   /* segment size in bytes, multiple of 128 in [256, 2^30]; 0 = automatic
+                             from the batch's size (256 B - 64 KiB) */
 } bmqcrc_opts;
 
 /* ---- scalar (host CPU) -------------------------------------------------- */
