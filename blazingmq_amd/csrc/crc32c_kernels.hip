@@ -425,13 +425,27 @@ struct PlanTotals {
     uint32_t total, identity, uni;
 };
 
-__device__ PlanTotals plan_totals(const BatchArgs& a, PlanLds* pl)
+// The loads are split from the reduction so that k_fold can issue them
+// together with its other prologue loads.
+struct PlanWords {
+    uint32_t v, nn, u, u0;
+};
+
+__device__ __forceinline__ PlanWords plan_load(const BatchArgs& a)
 {
     const uint32_t j = threadIdx.x, nb = a.nblocks;
-    const uint32_t v = j < nb ? a.block_sum[j] : 0u;
-    const uint32_t nn = j < nb ? a.block_sum[nb + j] : 0u;
-    const uint32_t u0 = a.block_sum[2u * nb];
-    const uint32_t u = j < nb ? a.block_sum[2u * nb + j] : u0;
+    PlanWords w;
+    w.v = j < nb ? a.block_sum[j] : 0u;
+    w.nn = j < nb ? a.block_sum[nb + j] : 0u;
+    w.u0 = a.block_sum[2u * nb];
+    w.u = j < nb ? a.block_sum[2u * nb + j] : w.u0;
+    return w;
+}
+
+__device__ PlanTotals plan_reduce(const BatchArgs& a, PlanLds* pl, const PlanWords w)
+{
+    const uint32_t j = threadIdx.x, nb = a.nblocks;
+    const uint32_t v = w.v, nn = w.nn, u = w.u, u0 = w.u0;
     const int ragged = __syncthreads_or(nn != 0u);
     const int mismatch = __syncthreads_or(u != u0);
     uint32_t ex;
@@ -446,6 +460,11 @@ __device__ PlanTotals plan_totals(const BatchArgs& a, PlanLds* pl)
     t.identity = ragged ? 0u : 1u;  // every message exactly one segment
     t.uni = (!mismatch && u0 != 0xffffffffu && u0 != 0u) ? u0 : 0u;
     return t;
+}
+
+__device__ __forceinline__ PlanTotals plan_totals(const BatchArgs& a, PlanLds* pl)
+{
+    return plan_reduce(a, pl, plan_load(a));
 }
 
 // Geometry of segment k of a message [mstart, mstart+len): byte range
@@ -523,19 +542,41 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     const uint32_t tab_lds = (uint32_t)(uintptr_t)(lds_u8*)lds;
     const uint32_t wave_lds = tab_lds + kTabBytes + wave * (kSlots * kSlotBytes);
 
-    // remainder-reduction tables -> LDS (8 KiB, once per block; no DMA in flight yet)
-    for (uint32_t t = threadIdx.x; t < 8u * 256u; t += blockDim.x) {
-        *(lds_u32*)(uintptr_t)(tab_lds + 4u * t) = c_ty[t >> 8][t & 255u];
+    // Prologue: every load that depends on nothing is issued before the first
+    // wait -- the remainder tables, k_plan's block words and the first group's
+    // descriptors as if segment = message (true for BMQCRC_F_WHOLE_MESSAGES
+    // and for identity batches; discarded otherwise).
+    static_assert(8 * 256 == 8 * kWavesPerBlock * 64, "table fill: 8 words per thread");
+    uint32_t tw[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t t = threadIdx.x + (uint32_t)i * (kWavesPerBlock * 64);
+        tw[i] = c_ty[t >> 8][t & 255u];
     }
-    __syncthreads();
+    const uint32_t whole = a.whole;
+    PlanWords pw = {0u, 0u, 0u, 0u};
+    if (!whole) {
+        pw = plan_load(a);
+    }
+    const uint32_t g0 = blockIdx.x * kWavesPerBlock + wave;
+    const uint32_t sid = g0 * 64u + (uint32_t)lane;
+    const SegDesc spec = fetch_desc(a, SegRef{sid, 0u}, sid < a.n);
+    // remainder-reduction tables -> LDS (8 KiB, once per block; no DMA in
+    // flight yet; plan_reduce's barriers order them before any lookup)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t t = threadIdx.x + (uint32_t)i * (kWavesPerBlock * 64);
+        *(lds_u32*)(uintptr_t)(tab_lds + 4u * t) = tw[i];
+    }
 
     // BMQCRC_F_WHOLE_MESSAGES: segment g = message g, one segment each, no
     // planner ran.  Otherwise the batch totals come from k_plan's block words.
     __shared__ PlanLds pl;
-    const uint32_t whole = a.whole;
     PlanTotals pt = {(uint32_t)a.n, 1u, 0u};
     if (!whole) {
-        pt = plan_totals(a, &pl);
+        pt = plan_reduce(a, &pl, pw);
+    } else {
+        __syncthreads();
     }
     const uint32_t total = pt.total;
     const uint32_t identity = pt.identity;
@@ -559,13 +600,17 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     // Descriptor pipeline across groups: the (message, part) of the group
     // after next and the (offset, length, seed) of the next group are loaded
     // while the current group folds, so no group starts on a cold load.
-    uint32_t g = blockIdx.x * kWavesPerBlock + wave;
+    uint32_t g = g0;
     SegDesc nxt = {0ull, 0u, 0u, 0u, 0u};
     SegRef ref2 = {0u, 0u};
     if (g < ngroups) {
         const uint32_t s0 = g * 64u + (uint32_t)lane;
-        nxt = fetch_desc(a, map_segment(a, &pl, s0, s0 < total, identity, uni, sorted),
-                         s0 < total);
+        if (identity) {  // whole or identity: the speculative descriptors are the ones
+            nxt = spec;
+        } else {
+            nxt = fetch_desc(a, map_segment(a, &pl, s0, s0 < total, identity, uni, sorted),
+                             s0 < total);
+        }
         const uint32_t s1 = (g + stride) * 64u + (uint32_t)lane;
         ref2 = map_segment(a, &pl, s1, g + stride < ngroups && s1 < total, identity, uni,
                            sorted);
