@@ -156,20 +156,46 @@ constexpr int kNTaps = BMQCRC_REL_NTAPS;
 //   Q_i = m_i ^ sum_{k in taps} Q_{i-32+k}
 // Slot (d+k)&31 is still the previous round's word when d+k < 32 and this
 // round's when d+k >= 32, exactly the recurrence.
-__device__ __forceinline__ void fold_round(uint32_t (&q)[32], const uint32_t (&m)[32])
+//
+// Seven tap pairs are adjacent (k, k+1); a second ring p holds
+// p[j] = Q_m ^ Q_{m+1} for the latest such m == j (mod 32), updated once per
+// word, so a word costs one pair update + 5 three-input XORs (m, 7 pairs,
+// 3 single taps) instead of 9.
+constexpr int kPairs[7] = {8, 10, 13, 18, 22, 25, 27};
+constexpr int kSingles[3] = {0, 6, 20};
+
+constexpr bool pairs_cover_taps()
+{
+    int n = 0;
+    for (int k = 0; k < 32; ++k) {
+        bool in_taps = false, covered = false;
+        for (int i = 0; i < kNTaps; ++i) {
+            in_taps = in_taps || kTaps[i] == k;
+        }
+        for (int i = 0; i < 3; ++i) {
+            covered = covered || kSingles[i] == k;
+        }
+        for (int i = 0; i < 7; ++i) {
+            covered = covered || kPairs[i] == k || kPairs[i] + 1 == k;
+        }
+        n += (in_taps != covered) ? 1 : 0;
+    }
+    return n == 0 && kNTaps == 3 + 2 * 7;
+}
+static_assert(pairs_cover_taps(), "tap pairs/singles must be exactly the relation's taps");
+
+__device__ __forceinline__ void fold_round(uint32_t (&q)[32], uint32_t (&p)[32],
+                                           const uint32_t (&m)[32])
 {
 #pragma unroll
     for (int d = 0; d < 32; ++d) {
-        uint32_t acc = m[d];
-        int i = 0;
-#pragma unroll
-        for (; i + 1 < kNTaps; i += 2) {
-            acc = xor3(acc, q[(d + kTaps[i]) & 31], q[(d + kTaps[i + 1]) & 31]);
-        }
-        if (i < kNTaps) {
-            acc ^= q[(d + kTaps[i]) & 31];
-        }
+        uint32_t acc = xor3(m[d], q[(d + kSingles[0]) & 31], q[(d + kSingles[1]) & 31]);
+        acc = xor3(acc, q[(d + kSingles[2]) & 31], p[(d + kPairs[0]) & 31]);
+        acc = xor3(acc, p[(d + kPairs[1]) & 31], p[(d + kPairs[2]) & 31]);
+        acc = xor3(acc, p[(d + kPairs[3]) & 31], p[(d + kPairs[4]) & 31]);
+        acc = xor3(acc, p[(d + kPairs[5]) & 31], p[(d + kPairs[6]) & 31]);
         q[d] = acc;
+        p[(d + 31) & 31] = q[(d + 31) & 31] ^ acc;
     }
 }
 
@@ -184,29 +210,39 @@ __device__ __forceinline__ uint32_t tab_lookup(uint32_t tab_lds, int k, uint32_t
     return *(const lds_u32*)(uintptr_t)(tab_lds + k * 1024u + b * 4u);
 }
 
-__device__ __forceinline__ uint32_t tail_round(const uint32_t (&q)[32], const uint32_t (&m)[32],
-                                               uint32_t tab_lds)
+__device__ __forceinline__ uint32_t tail_round(const uint32_t (&q)[32], const uint32_t (&p)[32],
+                                               const uint32_t (&m)[32], uint32_t tab_lds)
 {
+    // R_d = m_d ^ (taps that stay in the previous round: d + k <= 31); a pair
+    // (k, k+1) with d + k + 1 <= 31 is p[d + k]
     uint32_t R[32];
 #pragma unroll
     for (int d = 0; d < 32; ++d) {
-        uint32_t acc = m[d];
-        uint32_t pend = 0;
-        bool have = false;
+        uint32_t t[20];
+        int nt = 0;
+        t[nt++] = m[d];
 #pragma unroll
-        for (int i = 0; i < kNTaps; ++i) {
-            if (d + kTaps[i] <= 31) {
-                if (have) {
-                    acc = xor3(acc, pend, q[d + kTaps[i]]);
-                    have = false;
-                } else {
-                    pend = q[d + kTaps[i]];
-                    have = true;
-                }
+        for (int i = 0; i < 3; ++i) {
+            if (d + kSingles[i] <= 31) {
+                t[nt++] = q[d + kSingles[i]];
             }
         }
-        if (have) {
-            acc ^= pend;
+#pragma unroll
+        for (int i = 0; i < 7; ++i) {
+            if (d + kPairs[i] + 1 <= 31) {
+                t[nt++] = p[d + kPairs[i]];
+            } else if (d + kPairs[i] <= 31) {
+                t[nt++] = q[d + kPairs[i]];
+            }
+        }
+        uint32_t acc = t[0];
+        int i = 1;
+#pragma unroll
+        for (; i + 1 < nt; i += 2) {
+            acc = xor3(acc, t[i], t[i + 1]);
+        }
+        if (i < nt) {
+            acc ^= t[i];
         }
         R[d] = acc;
     }
@@ -669,10 +705,11 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         }
 
         // ------------------------------------------------------ fold rounds
-        uint32_t q[32];
+        uint32_t q[32], p[32];
 #pragma unroll
         for (int d = 0; d < 32; ++d) {
             q[d] = 0;
+            p[d] = 0;
         }
         uint32_t crc = 0;
         const uint32_t c0 = ~seed;
@@ -715,9 +752,9 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
                 dma_round<NT>(slot, pbase, plo, pcnt, zero, r + 2);
             }
             if (r + 1 < R) {
-                fold_round(q, m);
+                fold_round(q, p, m);
             } else {
-                crc = tail_round(q, m, tab_lds);  // every lane's last line: one tail per wave
+                crc = tail_round(q, p, m, tab_lds);  // every lane's last line: one tail per wave
             }
         }
 
@@ -744,6 +781,13 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         // can split its segments across a bucket boundary inside the wave),
         // so runs are delimited by a head ballot, never by key equality, and
         // a head stores plainly only when its run is the whole message.
+        if (__ballot(valid && nseg != 1u) == 0) {
+            // every segment of this group is a whole message: no runs to combine
+            if (valid) {
+                a.out[msg] = contrib;
+            }
+            continue;
+        }
         const uint32_t key = valid ? msg : 0xffffffffu;
         const uint32_t pkey = (uint32_t)__shfl_up((int)key, 1);
         const bool head = lane == 0 || pkey != key;

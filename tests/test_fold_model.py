@@ -154,3 +154,51 @@ def test_right_aligned_pieces_match_oracle(lead):
         padE = (off & ~127) + 128 * nl - (off + ln)
         got = G.mulmod_r(c, xpow(-8 * padE)) ^ 0xFFFFFFFF
         assert got == oracle.crc32c(arena[off:off + ln].tobytes(), seed), (off, ln, lead)
+
+
+# Tap pairing used by k_fold's fold_round / tail_round: adjacent taps (k, k+1)
+# are read from a second ring p[j] = Q_m ^ Q_{m+1}, updated once per word.
+PAIRS = [8, 10, 13, 18, 22, 25, 27]
+SINGLES = [0, 6, 20]
+
+
+def fold_stream_pairs(words):
+    q, p = [0] * 32, [0] * 32
+    nr = len(words) // 32
+    c = 0
+    for r in range(nr):
+        m = words[32 * r:32 * r + 32]
+        if r + 1 < nr:
+            for d in range(32):
+                acc = m[d]
+                for k in SINGLES:
+                    acc ^= q[(d + k) & 31]
+                for k in PAIRS:
+                    acc ^= p[(d + k) & 31]
+                q[d] = acc
+                p[(d + 31) & 31] = q[(d + 31) & 31] ^ acc
+        else:
+            for d in range(32):
+                acc = m[d]
+                for k in SINGLES:
+                    if d + k <= 31:
+                        acc ^= q[d + k]
+                for k in PAIRS:
+                    if d + k + 1 <= 31:
+                        acc ^= p[d + k]
+                    elif d + k <= 31:
+                        acc ^= q[d + k]
+                c = mul_y(c ^ acc)
+    return c
+
+
+def test_tap_pairs_cover_relation():
+    assert sorted(SINGLES + PAIRS + [k + 1 for k in PAIRS]) == sorted(TAPS)
+
+
+@pytest.mark.parametrize("rounds", [1, 2, 3, 7])
+def test_pair_ring_matches_plain_ring(rounds):
+    rng = np.random.default_rng(rounds)
+    for _ in range(20):
+        words = [int(w) for w in rng.integers(0, 1 << 32, size=32 * rounds, dtype=np.uint64)]
+        assert fold_stream_pairs(words) == fold_stream(words)

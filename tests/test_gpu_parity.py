@@ -362,3 +362,27 @@ def test_shape_hint_misprediction(cuda):
     mixed = np.concatenate([rng.integers(1, 1025, size=5120), rng.integers(0, 9000, size=3000)])
     for lens in (closed, mixed, closed, ragged, ragged, uniform, ragged, closed, mixed, closed):
         run(lens)
+
+
+def test_max_length_messages(cuda):
+    # The reference's length is an unsigned int (bmqp_crc32c.h:244-246), so the
+    # longest message is 2^32 - 1 bytes.  Two such messages (odd offsets,
+    # seeds, one overlapping the other) beside a short one, under the
+    # automatic shape and the smallest and largest segment sizes.
+    import torch
+    from blazingmq_amd import fill_synthetic
+    nbytes = (1 << 32) + 64
+    arena = torch.empty(nbytes, dtype=torch.uint8, device=cuda)
+    fill_synthetic(arena, 9)
+    offs = np.array([3, 0, 17], dtype=np.int64)
+    lens = np.array([0xFFFFFFFF, 1000, 0xFFFFFFFF - 16], dtype=np.uint32)
+    seeds = np.array([0x12345678, 0, 0xFFFFFFFF], dtype=np.uint32)
+    host = arena.cpu().numpy()
+    exp = oracle.batch(host, offs.astype(np.uint64), lens, seeds, nthreads=3)
+    del host
+    o = torch.from_numpy(offs).to(cuda)
+    ln = torch.from_numpy(lens.view(np.int32)).to(cuda)
+    sd = torch.from_numpy(seeds.view(np.int32)).to(cuda)
+    for seg in (0, 256, 1 << 30):
+        got = Crc32c.calculate_batch(arena, o, ln, sd, seg_bytes=seg).cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, exp), (seg, got, exp)
