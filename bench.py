@@ -79,6 +79,10 @@ def parse():
     p.add_argument("--msgs", type=int, default=0,
                    help="experiment: override the message count of a uniform config "
                         "(the line is then marked as not the BASELINE workload)")
+    p.add_argument("--shard", default="",
+                   help="experiment 'i/N': time only shard i of an N-way split of the config on "
+                        "this one GPU (a strong-scaling rank's work; the line is marked as not "
+                        "the BASELINE workload)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=2.0,
                    help="approximate wall time of the CPU-baseline sample")
@@ -174,7 +178,14 @@ def main():
         size = UNIFORM_SIZES[args.config]  # KeyError: only uniform configs can be resized
         gen = _uniform(args.msgs, size)
         desc = "EXPERIMENT (not the BASELINE workload): %d msgs x %d B" % (args.msgs, size)
-    lens_np, begin = gen(rank, world)
+    if args.shard:
+        if world > 1:
+            raise SystemExit("--shard is a one-process experiment")
+        si, sn = (int(x) for x in args.shard.split("/"))
+        lens_np, begin = gen(si, sn)
+        desc = "EXPERIMENT (not the BASELINE workload): shard %d of %d of %s" % (si, sn, desc)
+    else:
+        lens_np, begin = gen(rank, world)
     n = int(lens_np.size)
     offs_np = np.zeros(n, dtype=np.int64)
     if n > 1:
