@@ -482,19 +482,29 @@ __device__ PlanTotals plan_reduce(const BatchArgs& a, PlanLds* pl, const PlanWor
 {
     const uint32_t j = threadIdx.x, nb = a.nblocks;
     const uint32_t v = w.v, nn = w.nn, u = w.u, u0 = w.u0;
+    PlanTotals t;
+    // Closed forms need no offsets: one barrier for identity, two for uniform.
     const int ragged = __syncthreads_or(nn != 0u);
+    if (!ragged) {  // every message exactly one segment
+        t.total = (uint32_t)a.n;
+        t.identity = 1u;
+        t.uni = 1u;
+        return t;
+    }
     const int mismatch = __syncthreads_or(u != u0);
+    t.identity = 0u;
+    t.uni = (!mismatch && u0 != 0xffffffffu && u0 != 0u) ? u0 : 0u;
+    if (t.uni) {
+        t.total = (uint32_t)a.n * t.uni;
+        return t;
+    }
     uint32_t ex;
-    const uint32_t total = block_scan(v, &ex, pl->wsum);
+    t.total = block_scan(v, &ex, pl->wsum);
     if (j < nb) {
         pl->boff[j] = ex;
         pl->bu[j] = u;
     }
     __syncthreads();
-    PlanTotals t;
-    t.total = total;
-    t.identity = ragged ? 0u : 1u;  // every message exactly one segment
-    t.uni = (!mismatch && u0 != 0xffffffffu && u0 != 0u) ? u0 : 0u;
     return t;
 }
 
