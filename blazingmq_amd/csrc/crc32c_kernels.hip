@@ -199,6 +199,43 @@ __device__ __forceinline__ void fold_round(uint32_t (&q)[32], uint32_t (&p)[32],
     }
 }
 
+// First round of a stream (zero history, so the ring needs no clearing):
+// taps that reach the previous round read zero and are dropped at compile
+// time; p[31] pairs Q_-1 = 0 with Q_0.
+__device__ __forceinline__ void first_round(uint32_t (&q)[32], uint32_t (&p)[32],
+                                            const uint32_t (&m)[32])
+{
+#pragma unroll
+    for (int d = 0; d < 32; ++d) {
+        uint32_t t[11];
+        int nt = 0;
+        t[nt++] = m[d];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            if (d + kSingles[i] >= 32) {
+                t[nt++] = q[d + kSingles[i] - 32];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 7; ++i) {
+            if (d + kPairs[i] >= 31) {  // Q_(d+k-32) ^ Q_(d+k-31), Q_-1 = 0
+                t[nt++] = p[(d + kPairs[i]) & 31];
+            }
+        }
+        uint32_t acc = t[0];
+        int i = 1;
+#pragma unroll
+        for (; i + 1 < nt; i += 2) {
+            acc = xor3(acc, t[i], t[i + 1]);
+        }
+        if (i < nt) {
+            acc ^= t[i];
+        }
+        q[d] = acc;
+        p[(d + 31) & 31] = d == 0 ? acc : (q[d - 1] ^ acc);
+    }
+}
+
 // Final round: the last 32 words are the remainder coefficients R_d of the
 // stream modulo m(y).  Taps that would reach this round's (non-existent)
 // quotient words are dropped.  The remainder is reduced once per segment,
@@ -762,7 +799,11 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
                 dma_round<NT>(slot, pbase, plo, pcnt, zero, r + 2);
             }
             if (r + 1 < R) {
-                fold_round(q, p, m);
+                if (r == 0) {
+                    first_round(q, p, m);
+                } else {
+                    fold_round(q, p, m);
+                }
             } else {
                 crc = tail_round(q, p, m, tab_lds);  // every lane's last line: one tail per wave
             }

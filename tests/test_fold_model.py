@@ -202,3 +202,35 @@ def test_pair_ring_matches_plain_ring(rounds):
     for _ in range(20):
         words = [int(w) for w in rng.integers(0, 1 << 32, size=32 * rounds, dtype=np.uint64)]
         assert fold_stream_pairs(words) == fold_stream(words)
+
+
+def first_round_pairs(m):
+    """k_fold's first_round: zero history, taps into the previous round dropped."""
+    q, p = [0] * 32, [0] * 32
+    for d in range(32):
+        acc = m[d]
+        for k in SINGLES:
+            if d + k >= 32:
+                acc ^= q[d + k - 32]
+        for k in PAIRS:
+            if d + k >= 31:
+                acc ^= p[(d + k) & 31]
+        q[d] = acc
+        p[(d + 31) & 31] = acc if d == 0 else q[d - 1] ^ acc
+    return q, p
+
+
+def test_first_round_equals_fold_from_zero():
+    rng = np.random.default_rng(5)
+    for _ in range(50):
+        m = [int(w) for w in rng.integers(0, 1 << 32, size=32, dtype=np.uint64)]
+        q, p = [0] * 32, [0] * 32
+        for d in range(32):
+            acc = m[d]
+            for k in SINGLES:
+                acc ^= q[(d + k) & 31]
+            for k in PAIRS:
+                acc ^= p[(d + k) & 31]
+            q[d] = acc
+            p[(d + 31) & 31] = q[(d + 31) & 31] ^ acc
+        assert first_round_pairs(m) == (q, p)
