@@ -131,13 +131,26 @@ __device__ __forceinline__ uint32_t mersenne31(uint64_t x)
     return (x >= 0x7fffffffull) ? (uint32_t)(x - 0x7fffffffull) : (uint32_t)x;
 }
 
+// Wave-wide maximum by DPP (no LDS round trips): row_shr 1/2/4/8 leaves each
+// row's maximum in its lane 15, row_bcast 15/31 carries it across rows, lane
+// 63 ends with the wave's maximum.  Lanes without a source keep their own
+// value (old = v), which a maximum ignores.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_max(uint32_t v)
+{
+    return max(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, ROW_MASK, 0xf,
+                                                        false));
+}
+
 __device__ __forceinline__ uint32_t wave_max(uint32_t v)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        v = max(v, (uint32_t)__shfl_xor((int)v, o));
-    }
-    return __builtin_amdgcn_readfirstlane(v);
+    v = dpp_max<0x111, 0xf>(v);  // row_shr:1
+    v = dpp_max<0x112, 0xf>(v);  // row_shr:2
+    v = dpp_max<0x114, 0xf>(v);  // row_shr:4
+    v = dpp_max<0x118, 0xf>(v);  // row_shr:8
+    v = dpp_max<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
+    v = dpp_max<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
 __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src)
