@@ -72,7 +72,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--config", default="64k_x_64KiB", choices=list(CONFIGS))
+    p.add_argument("--config", default=None, choices=list(CONFIGS),
+                   help="default 64k_x_64KiB (the headline); --cpu-table: all configs")
     p.add_argument("--seg-bytes", type=int, default=0)
     p.add_argument("--whole-messages", action="store_true",
                    help="BMQCRC_F_WHOLE_MESSAGES: one lane per message, no planner launches")
@@ -92,9 +93,19 @@ def parse():
                         "GPU reaches steady-state clocks (measured: a cold GPU reads ~6%% low)")
     p.add_argument("--no-kernel-timing", action="store_true",
                    help="skip the HIP-event pass around k_fold (for external profilers)")
+    p.add_argument("--cpu-table", action="store_true",
+                   help="CPU baseline table (DESIGN.md section 6): every config, the three "
+                        "bdlde::Crc32c variants restated in oracle/, 1 and up to 16 threads")
+    p.add_argument("--protocol", action="store_true",
+                   help="measure the batch callers of SURVEY.md 8(f): partition recovery "
+                        "verify, deferred PUT-event CRCs, Blob batches, ledger validation")
     p.add_argument("--e2e", action="store_true",
                    help="end-to-end mode: H2D from pinned host + CRC + D2H (for DESIGN.md)")
-    return p.parse_args()
+    a = p.parse_args()
+    a.config_given = a.config is not None
+    if a.config is None:
+        a.config = "64k_x_64KiB"
+    return a
 
 
 def cpu_model():
@@ -140,6 +151,203 @@ def cpu_baseline(lens_np, seed, seconds):
     }
 
 
+CPU_VARIANTS = {"hw": "SSE4.2 crc32q 3-way interleaved (bdlde::Crc32c::calculate default)",
+                "hw_serial": "SSE4.2 crc32q serial (calculateHardwareSerial)",
+                "sw": "slicing-by-8 software (calculateSoftware)"}
+
+
+def cpu_table(args):
+    """CPU baseline table: the reference-equivalent CPU CRC32C (oracle/'s
+    restatement of bdlde::Crc32c, BDE 4.39 being unavailable offline), three
+    variants, 1 and T threads (one per core over byte-balanced message slices,
+    the reference's test5 pattern), each config sampled like the cpu_baseline
+    leg (first messages up to ~256 MiB).  One JSON line per measurement."""
+    import platform
+
+    import numpy as np
+    import oracle
+    threads = min(os.cpu_count() or 1, 16)
+    configs = [args.config] if args.config_given else list(CONFIGS)
+    for cfg in configs:
+        _, gen, seed, _ = CONFIGS[cfg]
+        lens_all, begin = gen(0, 1)
+        csum = np.cumsum(lens_all, dtype=np.uint64)
+        n = max(1, int(np.searchsorted(csum, 256 << 20, side="right")))
+        lens = np.ascontiguousarray(lens_all[:n])
+        offs = np.zeros(n, dtype=np.uint64)
+        if n > 1:
+            offs[1:] = csum[:n - 1]
+        nbytes = int(lens.sum(dtype=np.uint64))
+        arena = oracle.fill_payload(begin, nbytes, seed)
+        ref = oracle.batch(arena, offs, lens, nthreads=threads, variant="hw")
+        for var in CPU_VARIANTS:
+            assert np.array_equal(oracle.batch(arena, offs, lens, nthreads=threads,
+                                               variant=var), ref), (cfg, var)
+            for th in sorted({1, threads}):
+                t, _ = oracle.time_batch(arena, offs, lens, th, var, 1)
+                reps = max(1, int(args.cpu_seconds / 4 / max(t, 1e-6)))
+                t, _ = oracle.time_batch(arena, offs, lens, th, var, reps)
+                print(json.dumps({
+                    "config": cfg, "variant": var, "variant_desc": CPU_VARIANTS[var],
+                    "threads": th, "GiBps": round(nbytes / 2**30 * reps / t, 3),
+                    "sample_msgs": n, "sample_MiB": round(nbytes / 2**20, 1), "passes": reps,
+                    "host": cpu_model(), "nproc": os.cpu_count(),
+                    "machine": platform.machine()}), flush=True)
+
+
+def _wall(fn, reps):
+    """Median wall time of reps synchronous calls (after one warm-up call)."""
+    import time
+    fn()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return sorted(ts)[len(ts) // 2]
+
+
+def protocol(args):
+    """The batch callers of SURVEY.md 8(f), each timed end to end through its
+    C-ABI entry point on host buffers (host walk of the reference's format,
+    staging through HBM, one batched GPU call, results back), beside the
+    reference-equivalent CPU loop (host walk + one bdlde::Crc32c-equivalent
+    call per message, oracle/, 1 and 16 threads).  Parity: every stored CRC
+    verifies, planted corruptions are found, fills equal the CPU CRCs."""
+    import ctypes
+
+    import numpy as np
+    import oracle
+    import torch
+
+    from blazingmq_amd import _native as N
+    from blazingmq_amd import csl, put_event, storage, synth
+    threads = min(os.cpu_count() or 1, 16)
+    reps = max(3, args.steps // 4)
+
+    def cpu_leg(buf, offs, lens, walk_s):
+        out = {}
+        for th in (1, threads):
+            t, _ = oracle.time_batch(buf, offs, lens, th, "hw", 1)
+            k = max(1, int(0.5 / max(t, 1e-6)))
+            t, _ = oracle.time_batch(buf, offs, lens, th, "hw", k)
+            out["t%d_s" % th] = round(walk_s + t / k, 6)
+        return out
+
+    def line(path, ref, n, nbytes, gpu_s, walk_s, cpu, parity, note):
+        gib = nbytes / 2**30
+        print(json.dumps({
+            "path": path, "reference": ref, "messages": n, "payload_bytes": nbytes,
+            "gpu": {"s": round(gpu_s, 6), "GiBps": round(gib / gpu_s, 2), "includes": note},
+            "host_walk_s": round(walk_s, 6),
+            "cpu_baseline": {"kind": "port", "threads": [1, threads],
+                             "GiBps": [round(gib / cpu["t1_s"], 2),
+                                       round(gib / cpu["t%d_s" % threads], 2)],
+                             "what": "host walk + one SSE4.2 3-way CRC per message "
+                                     "(oracle/, bdlde::Crc32c analogue)"},
+            "speedup_vs_1_thread": round(cpu["t1_s"] / gpu_s, 2),
+            "parity": parity, "host": cpu_model()}), flush=True)
+
+    # 1. partition recovery (mqbs_filestore.cpp:2495-2624), 256K x 4000 B
+    n = args.msgs or 262144
+    journal, data, app_off, app_len = synth.partition(n, 4000)
+    walk_s = _wall(lambda: storage.scan_partition(journal, data), reps)
+    gpu_s = _wall(lambda: storage.verify_partition(journal, data), reps)
+    res = storage.verify_partition(journal, data)
+    bad = data.copy()
+    planted = [0, n // 2, n - 1]
+    for i in planted:
+        bad[int(app_off[i]) + 17] ^= 0x5A
+    found = storage.verify_partition(journal, bad)
+    jrec0 = journal.size - n * storage.JOURNAL_RECORD_SIZE
+    exp_off = [jrec0 + i * storage.JOURNAL_RECORD_SIZE for i in planted]
+    parity = {"n_bad": res["n_bad"], "planted": len(planted),
+              "found_exact": found["bad_record_offsets"].tolist() == exp_off}
+    line("recovery_verify", "mqbs::FileStore::recoverMessages CRC check "
+         "(mqbs_filestore.cpp:2495-2624)", n, int(app_len.sum(dtype=np.uint64)), gpu_s, walk_s,
+         cpu_leg(data, app_off, app_len, walk_s), parity,
+         "journal + DATA walk on the host, H2D of the DATA file, batched verify, D2H")
+    del journal, data, bad
+
+    # 2. deferred PUT-event CRCs (bmqp_puteventbuilder.cpp:302,320,400,413),
+    #    one 64 MiB-class event of 1 KiB messages
+    m = 60000
+    event, ev_off, ev_len = synth.put_event(m, 1020)
+    it = put_event.PutMessageIterator(event)
+    walk_s = _wall(lambda: it.scan(), reps)
+    opts = N.make_opts()
+    work = event.copy()
+
+    def fill():
+        N.check_count(N.lib.bmqcrc_put_event_fill_crcs(ctypes.c_void_p(work.ctypes.data),
+                                                       work.size, ctypes.byref(opts)))
+    gpu_s = _wall(fill, reps)
+    got = np.frombuffer(work.tobytes(), np.uint8)
+    pos = ev_off - 8
+    stored = (got[pos.astype(np.int64)[:, None] + np.arange(4)].astype(np.uint32)
+              * np.array([1 << 24, 1 << 16, 1 << 8, 1], np.uint32)).sum(1).astype(np.uint32)
+    exp = oracle.batch(event, ev_off, ev_len, nthreads=threads)
+    nm, nb, _ = put_event.PutMessageIterator(work).verify_crcs()
+    parity = {"fill_equals_cpu": bool(np.array_equal(stored, exp)), "verify_n_bad": nb}
+    line("put_event_fill_crcs", "bmqp::PutEventBuilder::packMessage CRC "
+         "(bmqp_puteventbuilder.cpp:302,320,400,413)", m, int(ev_len.sum()), gpu_s, walk_s,
+         cpu_leg(event, ev_off, ev_len, walk_s), parity,
+         "PUT walk on the host, H2D of the event, batched CRC, D2H, big-endian header writes")
+    del event, work
+
+    # 3. Blob batches (bmqp_crc32c.cpp:47-67): 16K blobs of 16 x 4 KiB buffers,
+    #    device-resident (buffers already in HBM)
+    dev = torch.device("cuda", 0)
+    nblob, nbuf, bsz = 16384, 16, 4096
+    total = nblob * nbuf * bsz
+    arena = torch.empty(total + 64, dtype=torch.uint8, device=dev)
+    from blazingmq_amd import fill_synthetic
+    fill_synthetic(arena, 21)
+    boff = torch.arange(nblob * nbuf, dtype=torch.int64, device=dev) * bsz
+    blen = torch.full((nblob * nbuf,), bsz, dtype=torch.int32, device=dev)
+    first = torch.arange(nblob + 1, dtype=torch.int64, device=dev) * nbuf
+    out = torch.empty(nblob, dtype=torch.int32, device=dev)
+    dopts = N.make_opts(flags=N.BMQCRC_F_DEVICE_PTRS)
+
+    def blobs():
+        N.check(N.lib.bmqcrc_crc32c_blobs(
+            ctypes.c_void_p(arena.data_ptr()), arena.numel(), ctypes.c_void_p(boff.data_ptr()),
+            ctypes.c_void_p(blen.data_ptr()), nblob * nbuf, ctypes.c_void_p(first.data_ptr()),
+            None, ctypes.c_void_p(out.data_ptr()), nblob, ctypes.byref(dopts)))
+        torch.cuda.synchronize(dev)
+    gpu_s = _wall(blobs, reps)
+    host = arena.cpu().numpy()
+    bo = np.arange(nblob, dtype=np.uint64) * (nbuf * bsz)
+    bl = np.full(nblob, nbuf * bsz, np.uint32)
+    exp = oracle.batch(host, bo, bl, nthreads=threads)  # a blob = its buffers concatenated
+    parity = {"equal": bool(np.array_equal(out.cpu().numpy().view(np.uint32), exp))}
+    line("blobs_device", "bmqp::Crc32c::calculate(const bdlbb::Blob&) per blob "
+         "(bmqp_crc32c.cpp:47-67)", nblob, total, gpu_s, 0.0, cpu_leg(host, bo, bl, 0.0), parity,
+         "device-resident buffers: per-buffer CRCs + on-device combine, one synchronous call")
+    del arena, host
+
+    # 4. cluster state ledger validation (mqbc_clusterstateledgerutil.cpp:248-336)
+    r = 32768
+    rng = np.random.default_rng(13)
+    adv = rng.integers(0, 256, size=(r, 1000), dtype=np.uint8)
+    log = np.frombuffer(csl.file_header(b"BMQ01") + b"".join(
+        csl.append_record(adv[i].tobytes(), sequence_number=i + 1) for i in range(r)),
+        np.uint8).copy()
+    wrc, end, roff, rlen, rcrc = csl.scan_log(log)
+    walk_s = _wall(lambda: csl.scan_log(log), reps)
+    gpu_s = _wall(lambda: csl.validate_log(log), reps)
+    rc, off, _ = csl.validate_log(log)
+    bad = log.copy()
+    bad[int(roff[r // 3]) + 40] ^= 1
+    rc_bad, _, first_bad = csl.validate_log(bad)
+    parity = {"rc": rc, "end_offset_ok": off == log.size, "corrupt_rc": rc_bad,
+              "first_bad_ok": first_bad == int(roff[r // 3])}
+    line("csl_validate", "mqbc::ClusterStateLedgerUtil::validateLog "
+         "(mqbc_clusterstateledgerutil.cpp:248-336)", r, int(np.asarray(rlen).sum()), gpu_s,
+         walk_s, cpu_leg(log, np.asarray(roff, np.uint64), np.asarray(rlen, np.uint32), walk_s),
+         parity, "ledger walk on the host, H2D, batched verify, D2H")
+
+
 def pmc_traffic(config):
     """HBM bytes per k_fold launch from the newest committed rocprofv3 PMC
     summary of this config (profiles/rNN/<config>_summary.json): read =
@@ -155,6 +363,12 @@ def pmc_traffic(config):
 
 def main():
     args = parse()
+    if args.cpu_table:
+        return cpu_table(args)
+    if args.protocol:
+        import torch
+        torch.cuda.set_device(0)
+        return protocol(args)
     import numpy as np
     import torch
     import torch.distributed as dist
