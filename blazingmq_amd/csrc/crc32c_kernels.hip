@@ -11,8 +11,9 @@
 //   * The fold is table-less: the minimal polynomial of y = x^32 mod P,
 //     m(y) = y^32 + sum_{k in REL_TAPS} y^k, vanishes mod P, so the word
 //     stream is reduced modulo m(y) by a 17-tap Fibonacci recurrence over a
-//     32-word register ring -- 9 v_bitop3 (3-input XOR) per word, no
-//     carry-less multiply, no lookup table.
+//     32-word register ring -- 6 VALU per word (seven adjacent tap pairs come
+//     from a second ring of pair XORs), no carry-less multiply, no lookup
+//     table.
 //   * Only the last 32 remainder words get a real GF(2) reduction (Horner by
 //     x^32 with slicing tables in LDS), once per segment.
 //   * Bytes reach the lanes through LDS: per round a wave DMAs (LDS-DMA,
