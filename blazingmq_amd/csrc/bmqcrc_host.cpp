@@ -434,6 +434,11 @@ int check_ranges(const uint64_t* offsets, const uint32_t* lengths, uint64_t n,
     return 0;
 }
 
+int verify_locked(Ctx& c, Workspace* w, const bmqcrc_opts& o, uint32_t seg, bool arena_staged,
+                  const void* arena, uint64_t arena_bytes, const uint64_t* offsets,
+                  const uint32_t* lengths, const uint32_t* expected, uint64_t n, uint64_t* n_bad,
+                  uint64_t* bad_idx, uint64_t bad_cap);
+
 }  // namespace
 
 extern "C" int bmqcrc_set_error(int rc, const char* msg)
@@ -530,6 +535,24 @@ int bmqcrc_crc32c_verify(const void* arena, uint64_t arena_bytes, const uint64_t
     }
     Workspace* w = c.w;
     std::lock_guard<std::mutex> g(w->mu);
+    return verify_locked(c, w, o, seg, false, arena, arena_bytes, offsets, lengths, expected, n,
+                         n_bad, bad_idx, bad_cap);
+}
+
+}  // extern "C"
+
+namespace {
+
+// The verify pipeline after the workspace lock: stage (host buffers; the
+// arena may already be staged), fold, compare on the device, collect the
+// lowest mismatching indices.
+int verify_locked(Ctx& c, Workspace* w, const bmqcrc_opts& o, uint32_t seg, bool arena_staged,
+                  const void* arena, uint64_t arena_bytes, const uint64_t* offsets,
+                  const uint32_t* lengths, const uint32_t* expected, uint64_t n, uint64_t* n_bad,
+                  uint64_t* bad_idx, uint64_t bad_cap)
+{
+    int rc;
+    const bool dev_ptrs = (o.flags & BMQCRC_F_DEVICE_PTRS) != 0;
     const uint32_t cap = (uint32_t)std::min<uint64_t>(bad_cap, 1u << 24);
     if ((rc = w->out.ensure(4 * n)) || (rc = w->vcount.ensure(4)) ||
         (rc = w->vidx.ensure(4ull * std::max<uint32_t>(cap, 1)))) {
@@ -540,7 +563,7 @@ int bmqcrc_crc32c_verify(const void* arena, uint64_t arena_bytes, const uint64_t
     const uint32_t* d_len = lengths;
     const uint32_t* d_exp = expected;
     if (!dev_ptrs) {
-        if ((rc = stage(c, w->arena, arena, arena_bytes)) ||
+        if ((!arena_staged && (rc = stage(c, w->arena, arena, arena_bytes))) ||
             (rc = stage(c, w->offsets, offsets, 8 * n)) ||
             (rc = stage(c, w->lengths, lengths, 4 * n)) ||
             (rc = stage(c, w->expected, expected, 4 * n))) {
@@ -604,6 +627,82 @@ int bmqcrc_crc32c_verify(const void* arena, uint64_t arena_bytes, const uint64_t
     }
     return 0;
 }
+
+
+}  // namespace
+
+int bmqcrc_verify_host_overlapped(const void* arena, uint64_t arena_bytes,
+                                  bmqcrc_prepare_fn prepare, void* pctx, uint64_t* n_bad,
+                                  std::vector<uint64_t>* bad, uint64_t bad_cap,
+                                  const bmqcrc_opts* opts)
+{
+    t_err.clear();
+    if (!n_bad || !prepare || !bad || (!arena && arena_bytes)) {
+        return fail(BMQCRC_EINVAL, "null pointer argument");
+    }
+    *n_bad = 0;
+    bmqcrc_opts o;
+    uint32_t seg;
+    int dev, rc;
+    if ((rc = parse_opts(opts, &o, &seg, &dev))) {
+        return rc;
+    }
+    if (o.flags & (BMQCRC_F_DEVICE_PTRS | BMQCRC_F_ASYNC)) {
+        return fail(BMQCRC_EINVAL, "overlapped verify takes host buffers, synchronously");
+    }
+    const uint64_t* off = nullptr;
+    const uint32_t* len = nullptr;
+    const uint32_t* exp = nullptr;
+    uint64_t n = 0;
+    Ctx c;
+    if ((rc = open_ctx(dev, o.stream, &c))) {
+        // no usable device: a malformed input is still reported first
+        const std::string why = t_err;
+        const int prc = prepare(pctx, &off, &len, &exp, &n);
+        if (prc || n == 0) {  // nothing to verify needs no device
+            return prc;
+        }
+        return fail(rc, why);
+    }
+    Workspace* w = c.w;
+    std::lock_guard<std::mutex> g(w->mu);
+    // The arena's H2D copy runs on a helper thread while the caller's walk
+    // produces the descriptors on this one (its errors stay in this thread's
+    // bmqcrc_last_error).
+    int src = 0;
+    std::thread copier([&] {
+        if (hipSetDevice(dev) != hipSuccess) {
+            src = BMQCRC_EIO;
+            return;
+        }
+        src = stage(c, w->arena, arena, arena_bytes);
+        if (!src && hipStreamSynchronize(c.s) != hipSuccess) {
+            src = BMQCRC_EIO;
+        }
+    });
+    const int prc = prepare(pctx, &off, &len, &exp, &n);
+    copier.join();
+    if (prc) {
+        return prc;
+    }
+    if (src) {
+        return fail(src, "staging the arena to the device failed");
+    }
+    if (n == 0) {
+        return 0;
+    }
+    if (n > 0xFFFFFFFFull) {
+        return fail(BMQCRC_EINVAL, "at most 2^32-1 messages per batch");
+    }
+    if ((rc = check_ranges(off, len, n, arena_bytes))) {
+        return rc;
+    }
+    bad->assign(std::min<uint64_t>(bad_cap, n), 0);
+    return verify_locked(c, w, o, seg, true, arena, arena_bytes, off, len, exp, n, n_bad,
+                         bad->data(), bad->size());
+}
+
+extern "C" {
 
 int bmqcrc_crc32c_blobs(const void* arena, uint64_t arena_bytes, const uint64_t* buf_offsets,
                         const uint32_t* buf_lengths, uint64_t nbuf,

@@ -85,6 +85,21 @@ extern "C" __attribute__((visibility("hidden"))) int bmqcrc_launch_compare_order
                                             uint64_t n, uint32_t* block_cnt, uint32_t nblocks,
                                             uint32_t* bad_idx, uint32_t bad_cap, int pass,
                                             void* stream);
+// Host-buffer verify with the descriptor walk overlapped (bmqcrc_host.cpp):
+// `prepare` runs on the calling thread while the arena is copied to the device
+// on a helper thread; it returns 0 and the (offset, length, expected CRC)
+// arrays of n messages, or a BMQCRC_E* code with the error already set.
+typedef int (*bmqcrc_prepare_fn)(void* ctx, const uint64_t** offsets, const uint32_t** lengths,
+                                 const uint32_t** expected, uint64_t* n);
+// `bad` receives the lowest min(bad_cap, n) mismatching indices' slots (the
+// first min(*n_bad, size) are valid), like bmqcrc_crc32c_verify.  C++ only.
+#ifdef __cplusplus
+#include <vector>
+struct bmqcrc_opts;
+__attribute__((visibility("hidden"))) int bmqcrc_verify_host_overlapped(
+    const void* arena, uint64_t arena_bytes, bmqcrc_prepare_fn prepare, void* pctx,
+    uint64_t* n_bad, std::vector<uint64_t>* bad, uint64_t bad_cap, const bmqcrc_opts* opts);
+#endif
 // Thread-local error message shared by every C-ABI source (bmqcrc_last_error).
 extern "C" __attribute__((visibility("hidden"))) int bmqcrc_set_error(int rc, const char* msg);
 extern "C" __attribute__((visibility("hidden"))) void bmqcrc_clear_error(void);

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <string>
+#include <functional>
 #include <vector>
 
 #include "../../include/bmqcrc.h"
@@ -286,17 +287,40 @@ int host_opts(const bmqcrc_opts* in, bmqcrc_opts* o)
     return 0;
 }
 
-int verify_ranges(const void* arena, uint64_t bytes, const Ranges& r, uint64_t* n_bad,
-                  std::vector<uint64_t>* bad, uint64_t bad_cap, const bmqcrc_opts* opts)
+// The walk of a verify call, run by bmqcrc_verify_host_overlapped while the
+// buffer is copied to the device.
+struct Overlap {
+    std::function<int(Ranges*)> walk;
+    Ranges r;
+    bool walked = false;  // the walk succeeded
+};
+
+int overlap_prepare(void* p, const uint64_t** off, const uint32_t** len, const uint32_t** exp,
+                    uint64_t* n)
+{
+    Overlap* o = (Overlap*)p;
+    const int rc = o->walk(&o->r);
+    if (rc) {
+        return rc;
+    }
+    o->walked = true;
+    *off = o->r.off.data();
+    *len = o->r.len.data();
+    *exp = o->r.crc.data();
+    *n = o->r.off.size();
+    return 0;
+}
+
+int verify_overlapped(const void* arena, uint64_t bytes, Overlap* ov, uint64_t* n_bad,
+                      std::vector<uint64_t>* bad, uint64_t bad_cap, const bmqcrc_opts* opts)
 {
     bmqcrc_opts o;
     int rc;
     if ((rc = host_opts(opts, &o))) {
         return rc;
     }
-    bad->assign(std::min<uint64_t>(bad_cap, r.off.size()), 0);
-    return bmqcrc_crc32c_verify(arena, bytes, r.off.data(), r.len.data(), r.crc.data(),
-                                r.off.size(), n_bad, bad->data(), bad->size(), &o);
+    return bmqcrc_verify_host_overlapped(arena, bytes, overlap_prepare, ov, n_bad, bad, bad_cap,
+                                         &o);
 }
 
 }  // namespace
@@ -351,14 +375,12 @@ int bmqcrc_put_event_verify(const void* event, uint64_t len, uint64_t* n_msgs, u
         return bmqcrc_set_error(BMQCRC_EINVAL, "null pointer argument");
     }
     *n_msgs = *n_bad = 0;
-    Ranges r;
-    int rc = walk_put_event((const uint8_t*)event, len, &r);
-    if (rc) {
-        return rc;
-    }
-    *n_msgs = r.off.size();
+    Overlap ov;  // the event's copy to the device overlaps the walk
+    ov.walk = [&](Ranges* r) { return walk_put_event((const uint8_t*)event, len, r); };
     std::vector<uint64_t> bad;
-    if ((rc = verify_ranges(event, len, r, n_bad, &bad, bad_cap, opts))) {
+    const int rc = verify_overlapped(event, len, &ov, n_bad, &bad, bad_cap, opts);
+    *n_msgs = ov.walked ? ov.r.off.size() : 0;
+    if (rc) {
         return rc;
     }
     std::copy(bad.begin(), bad.begin() + std::min<uint64_t>(*n_bad, bad.size()), bad_idx);
@@ -388,14 +410,16 @@ int bmqcrc_recover_verify(const void* journal, uint64_t jlen, const void* data, 
         return bmqcrc_set_error(BMQCRC_EINVAL, "null pointer argument");
     }
     *n_msgs = *n_bad = 0;
-    Ranges r;
-    int rc = walk_partition((const uint8_t*)journal, jlen, (const uint8_t*)data, dlen, &r);
-    if (rc) {
-        return rc;
-    }
-    *n_msgs = r.off.size();
+    // the DATA file's copy to the device overlaps the journal walk
+    Overlap ov;
+    ov.walk = [&](Ranges* r) {
+        return walk_partition((const uint8_t*)journal, jlen, (const uint8_t*)data, dlen, r);
+    };
     std::vector<uint64_t> bad;
-    if ((rc = verify_ranges(data, dlen, r, n_bad, &bad, bad_cap, opts))) {
+    const int rc = verify_overlapped(data, dlen, &ov, n_bad, &bad, bad_cap, opts);
+    const Ranges& r = ov.r;
+    *n_msgs = ov.walked ? r.off.size() : 0;
+    if (rc) {
         return rc;
     }
     const uint64_t k = std::min<uint64_t>(*n_bad, bad.size());
@@ -426,18 +450,20 @@ int bmqcrc_csl_validate(const void* log, uint64_t len, const uint8_t* expected_l
     if ((!log && len) || !csl_rc || !offset) {
         return bmqcrc_set_error(BMQCRC_EINVAL, "null pointer argument");
     }
-    Ranges r;
     int walk_rc = 0;
     uint64_t end = 0;
-    walk_csl((const uint8_t*)log, len, expected_log_id, &r, &walk_rc, &end);
+    Overlap ov;  // the log's copy to the device overlaps the walk
+    ov.walk = [&](Ranges* r) {
+        walk_csl((const uint8_t*)log, len, expected_log_id, r, &walk_rc, &end);
+        return 0;
+    };
     uint64_t n_bad = 0;
     std::vector<uint64_t> bad;
-    if (!r.off.empty()) {
-        const int rc = verify_ranges(log, len, r, &n_bad, &bad, 1, opts);
-        if (rc) {
-            return rc;
-        }
+    const int rc = verify_overlapped(log, len, &ov, &n_bad, &bad, 1, opts);
+    if (rc) {
+        return rc;
     }
+    const Ranges& r = ov.r;
     // The reference stops at the first failing record in log order: every
     // record gathered precedes the point where the walk itself stopped.
     if (n_bad) {
