@@ -634,13 +634,15 @@ int verify_locked(Ctx& c, Workspace* w, const bmqcrc_opts& o, uint32_t seg, bool
 int bmqcrc_verify_host_overlapped(const void* arena, uint64_t arena_bytes,
                                   bmqcrc_prepare_fn prepare, void* pctx, uint64_t* n_bad,
                                   std::vector<uint64_t>* bad, uint64_t bad_cap,
-                                  const bmqcrc_opts* opts)
+                                  const bmqcrc_opts* opts, std::vector<uint32_t>* crcs)
 {
     t_err.clear();
-    if (!n_bad || !prepare || !bad || (!arena && arena_bytes)) {
+    if (!prepare || (!crcs && (!n_bad || !bad)) || (!arena && arena_bytes)) {
         return fail(BMQCRC_EINVAL, "null pointer argument");
     }
-    *n_bad = 0;
+    if (n_bad) {
+        *n_bad = 0;
+    }
     bmqcrc_opts o;
     uint32_t seg;
     int dev, rc;
@@ -696,6 +698,21 @@ int bmqcrc_verify_host_overlapped(const void* arena, uint64_t arena_bytes,
     }
     if ((rc = check_ranges(off, len, n, arena_bytes))) {
         return rc;
+    }
+    if (crcs) {  // compute: stage the descriptors, fold, copy the CRCs back
+        crcs->assign(n, 0);
+        if ((rc = stage(c, w->offsets, off, 8 * n)) || (rc = stage(c, w->lengths, len, 4 * n)) ||
+            (rc = w->out.ensure(4 * n))) {
+            return rc;
+        }
+        if ((rc = run_batch(c, o.flags, seg, w->arena.p, arena_bytes,
+                            (const uint64_t*)w->offsets.p, (const uint32_t*)w->lengths.p, nullptr,
+                            (uint32_t*)w->out.p, n))) {
+            return rc;
+        }
+        HIP_TRY(hipMemcpyAsync(crcs->data(), w->out.p, 4 * n, hipMemcpyDeviceToHost, c.s));
+        HIP_TRY(hipStreamSynchronize(c.s));
+        return 0;
     }
     bad->assign(std::min<uint64_t>(bad_cap, n), 0);
     return verify_locked(c, w, o, seg, true, arena, arena_bytes, off, len, exp, n, n_bad,

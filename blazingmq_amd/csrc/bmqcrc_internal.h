@@ -92,13 +92,16 @@ extern "C" __attribute__((visibility("hidden"))) int bmqcrc_launch_compare_order
 typedef int (*bmqcrc_prepare_fn)(void* ctx, const uint64_t** offsets, const uint32_t** lengths,
                                  const uint32_t** expected, uint64_t* n);
 // `bad` receives the lowest min(bad_cap, n) mismatching indices' slots (the
-// first min(*n_bad, size) are valid), like bmqcrc_crc32c_verify.  C++ only.
+// first min(*n_bad, size) are valid), like bmqcrc_crc32c_verify.  With `crcs`
+// non-null the call computes instead of verifying: crcs = the n CRCs
+// (expected, n_bad and bad are then unused).  C++ only.
 #ifdef __cplusplus
 #include <vector>
 struct bmqcrc_opts;
 __attribute__((visibility("hidden"))) int bmqcrc_verify_host_overlapped(
     const void* arena, uint64_t arena_bytes, bmqcrc_prepare_fn prepare, void* pctx,
-    uint64_t* n_bad, std::vector<uint64_t>* bad, uint64_t bad_cap, const bmqcrc_opts* opts);
+    uint64_t* n_bad, std::vector<uint64_t>* bad, uint64_t bad_cap, const bmqcrc_opts* opts,
+    std::vector<uint32_t>* crcs = nullptr);
 #endif
 // Thread-local error message shared by every C-ABI source (bmqcrc_last_error).
 extern "C" __attribute__((visibility("hidden"))) int bmqcrc_set_error(int rc, const char* msg);

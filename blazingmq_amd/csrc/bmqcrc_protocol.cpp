@@ -345,21 +345,20 @@ int64_t bmqcrc_put_event_fill_crcs(void* event, uint64_t len, const bmqcrc_opts*
     if (!event && len) {
         return bmqcrc_set_error(BMQCRC_EINVAL, "null event");
     }
-    Ranges r;
     bmqcrc_opts o;
     int rc;
-    if ((rc = walk_put_event((const uint8_t*)event, len, &r)) || (rc = host_opts(opts, &o))) {
+    if ((rc = host_opts(opts, &o))) {
         return rc;
     }
+    Overlap ov;  // the event's copy to the device overlaps the walk
+    ov.walk = [&](Ranges* r) { return walk_put_event((const uint8_t*)event, len, r); };
+    std::vector<uint32_t> out;
+    if ((rc = bmqcrc_verify_host_overlapped(event, len, overlap_prepare, &ov, nullptr, nullptr, 0,
+                                            &o, &out))) {
+        return rc;
+    }
+    const Ranges& r = ov.r;
     const uint64_t n = r.off.size();
-    if (n == 0) {
-        return 0;
-    }
-    std::vector<uint32_t> out(n);
-    if ((rc = bmqcrc_crc32c_batch(event, len, r.off.data(), r.len.data(), nullptr, out.data(), n,
-                                  &o))) {
-        return rc;
-    }
     uint8_t* ev = (uint8_t*)event;
     for (uint64_t i = 0; i < n; ++i) {
         put_be32(ev + r.pos[i], out[i]);
