@@ -1239,14 +1239,24 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_sort(BatchArgs a)
                 pos = atomicAdd(&run[c_full], tf);
             }
             pos = (uint32_t)__shfl((int)pos, 0) + (x - nf_all);
+            // the whole wave writes each lane's runs in turn (coalesced),
+            // instead of every lane looping over its own runs while the
+            // others wait on the longest
+            const uint32_t lane0 = threadIdx.x & ~63u;
+            for (uint64_t busy = __ballot(nf_all != 0u); busy; busy &= busy - 1ull) {
+                const int src = __builtin_ctzll(busy);
+                uint32_t at = (uint32_t)__builtin_amdgcn_readlane((int)pos, src);
 #pragma unroll
-            for (uint32_t v = 0; v < kPlanV; ++v) {
-                const uint64_t i = base + (uint64_t)v * kPlanBlock + threadIdx.x;
-                const uint32_t nf = nseg[v] ? nseg[v] - 1u : 0u;
-                for (uint32_t k = 0; k < nf; ++k) {
-                    info[pos + k] = make_uint2((uint32_t)i, k);
+                for (uint32_t v = 0; v < kPlanV; ++v) {
+                    const uint32_t nf = (uint32_t)__builtin_amdgcn_readlane(
+                        (int)(nseg[v] ? nseg[v] - 1u : 0u), src);
+                    const uint32_t i =
+                        (uint32_t)(base + (uint64_t)v * kPlanBlock + lane0 + (uint32_t)src);
+                    for (uint32_t k = (uint32_t)lane; k < nf; k += 64u) {
+                        info[at + k] = make_uint2(i, k);
+                    }
+                    at += nf;
                 }
-                pos += nf;
             }
         }
         // last (or only) segments: per class, one LDS atomic per wave and tile
