@@ -80,7 +80,7 @@ struct DevBuf {
 // Planner + staging scratch for one (device, stream).
 struct Workspace {
     std::mutex mu;
-    DevBuf seg_first, block_sum, seginfo, bhist, ctrl;
+    DevBuf seg_first, block_sum, seginfo, bhist;
     // host-pointer staging
     DevBuf arena, offsets, lengths, seeds, out;
     // verify / blobs
@@ -89,7 +89,7 @@ struct Workspace {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timing, spare;
     // Shape of the last batch planned on this workspace, written by k_fold
     // into host-mapped memory (kHint*): after a closed-form batch the next
-    // one skips the k_plan_hist/k_plan_sort launches.  A wrong guess only
+    // one skips the size-class histogram and the k_plan_sort launch.  A wrong guess only
     // costs speed (k_fold then maps segments by binary search).
     uint32_t* hint_host = nullptr;
     uint32_t* hint_dev = nullptr;
@@ -193,13 +193,8 @@ int plan_ws(Workspace* w, uint64_t n, uint64_t arena_bytes, uint32_t seg, BatchA
     if ((rc = w->seg_first.ensure(4 * std::max<uint64_t>(n, 1))) ||
         (rc = w->block_sum.ensure(12ull * kPlanMaxBlocks)) ||
         (rc = w->seginfo.ensure(8 * max_segs)) ||
-        (rc = w->bhist.ensure(4ull * kBuckets * kPlanMaxBlocks)) ||
-        (rc = w->ctrl.ensure(sizeof(PlanCtrl)))) {
+        (rc = w->bhist.ensure(4ull * kBuckets * kPlanMaxBlocks))) {
         return rc;
-    }
-    if (w->ctrl.fresh) {
-        // last-block-done tickets must start at zero (the kernels reset them)
-        HIP_TRY(hipMemset(w->ctrl.p, 0, w->ctrl.bytes));
     }
     if (!w->hint_host) {
         void* h = nullptr;
@@ -221,7 +216,6 @@ int plan_ws(Workspace* w, uint64_t n, uint64_t arena_bytes, uint32_t seg, BatchA
     a->block_sum = (uint32_t*)w->block_sum.p;
     a->seginfo = (uint32_t*)w->seginfo.p;
     a->bhist = (uint32_t*)w->bhist.p;
-    a->ctrl = (PlanCtrl*)w->ctrl.p;
     a->max_segs = max_segs;
     return 0;
 }

@@ -19,17 +19,6 @@ constexpr int kPlanMaxBlocks = 256;  // planner grids: contiguous message ranges
 
 constexpr int kBuckets = 16;            // segment size classes: floor(log2(lines))
 
-// Control words of the segment-map launches (device memory).  The batch
-// totals (segment count, identity / uniform shape, block offsets) are not
-// stored: every consumer kernel derives them in its prologue from k_plan's
-// per-block words (block_sum), see plan_totals() in crc32c_kernels.hip.
-struct PlanCtrl {
-    uint32_t sorted;       // 1: seginfo lists the segments grouped by size class
-                           //    (written by k_plan_hist's last block, ragged batches only)
-    uint32_t ticket_hist;  // last-block-done ticket of k_plan_hist (zeroed at allocation,
-                           //    reset by the last block)
-};
-
 struct BatchArgs {
     const uint8_t* arena;      // device
     const uint64_t* offsets;   // device, n
@@ -41,8 +30,7 @@ struct BatchArgs {
                                // messages with != 1 segment | segments per message if equal
                                // for all the block's messages, else ~0]
     uint32_t* seginfo;         // workspace, 2 * max_segs: (message, k) in size-class order
-    uint32_t* bhist;           // workspace, kBuckets * nblocks: histogram, then offsets
-    PlanCtrl* ctrl;            // workspace
+    uint32_t* bhist;           // workspace, kBuckets * nblocks: per-block size-class histogram
     uint64_t n;
     uint64_t max_segs;
     uint64_t per_msg;          // messages per planner block (multiple of kPlanBlock)
@@ -52,11 +40,11 @@ struct BatchArgs {
     uint32_t blocks_per_cu;    // k_fold grid: 1 (large messages) or 2 blocks per CU
     uint32_t tune;             // experiment knobs (BMQCRC_TUNE env): bit0 disables nt LDS-DMA
                                // loads, bit1 forces a 1-block/CU grid, bit3 forces 2, bit4
-                               // always launches k_plan_hist/k_plan_sort
-    uint32_t map_planned;      // 1: k_plan_hist/k_plan_sort run before k_fold; 0: they
-                               //    were skipped (the previous batch on this workspace was
-                               //    closed-form) and a ragged batch maps segments by binary
-                               //    search instead -- slower, never wrong
+                               // always builds the histogram and launches k_plan_sort
+    uint32_t map_planned;      // 1: k_plan builds the size-class histogram and k_plan_sort
+                               //    runs before k_fold; 0: skipped (the previous batch on this
+                               //    workspace was closed-form) and a ragged batch maps segments
+                               //    by binary search instead -- slower, never wrong
     uint32_t* shape_hint;      // host-mapped word or nullptr: k_fold writes kHintClosed or
                                // kHintRagged, the host reads it when planning the next batch
 };

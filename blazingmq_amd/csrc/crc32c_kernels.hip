@@ -678,8 +678,10 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     const uint32_t total = pt.total;
     const uint32_t identity = pt.identity;
     const uint32_t uni = pt.uni;
-    // the size-class order exists only if k_plan_hist/k_plan_sort ran
-    const uint32_t sorted = (whole || !a.map_planned || identity || uni) ? 0u : a.ctrl->sorted;
+    // the size-class order exists only if the histogram and k_plan_sort ran
+    // (and seginfo could hold every segment)
+    const uint32_t sorted =
+        (whole || !a.map_planned || identity || uni || total > a.max_segs) ? 0u : 1u;
     const uint32_t ngroups = (total + 63u) / 64u;
     const uint32_t SEG = a.seg_bytes;
     const uint64_t arena = (uint64_t)(uintptr_t)a.arena;
@@ -878,33 +880,33 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
 }
 
 // ---------------------------------------------------------------- planner
-// Last-block-done hand-off without fences (MI355X_MICROARCH.md "Workgroup
-// dispatch ... visibility", valid forms, write-through row): thread 0 of every
-// block publishes its words with agent-scope relaxed (sc1, write-through)
-// stores, waits vmcnt(0), then takes a relaxed agent ticket; the block that
-// draws the last ticket reads the published words with sc1 loads only.
-__device__ __forceinline__ void publish(uint32_t* p, uint32_t v)
+// Two classes per octave of the line count (1, 2, 3, 4-5, 6-7, 8-11, 12-15,
+// ..., 128-191, >= 192): lanes of a wave differ by at most 1.5x in rounds.
+// 16 buckets cover the default 16 KiB segments (<= 129 lines).
+__device__ __forceinline__ uint32_t size_class(uint32_t nl)
 {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    nl |= 1u;
+    const uint32_t b = 31u - __clz(nl);
+    const uint32_t c = b ? 2u * b + ((nl >> (b - 1u)) & 1u) : 0u;
+    return c < kBuckets - 1 ? c : kBuckets - 1;
 }
 
-__device__ __forceinline__ uint32_t consume(const uint32_t* p)
+// Segments of a message (offset off, length len) and the size class of its
+// last (or only) one.  Every other segment spans exactly seg_bytes / 128
+// lines (internal boundaries are 128-byte aligned and seg_bytes is a multiple
+// of 128), so it is in class size_class(seg_bytes / 128).
+__device__ __forceinline__ uint32_t msg_segments(const BatchArgs& a, uint64_t off, uint32_t len,
+                                                 uint32_t seg_shift, uint32_t* c_last)
 {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Called by all threads after thread 0 has published.  True in the last block.
-__device__ __forceinline__ bool last_block_arrival(uint32_t* ticket, uint32_t nblocks,
-                                                   uint32_t* flag_lds)
-{
-    if (threadIdx.x == 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t t =
-            __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *flag_lds = (t == nblocks - 1) ? 1u : 0u;
+    *c_last = kBuckets;  // kBuckets: no segment
+    if (len == 0) {
+        return 0;
     }
-    __syncthreads();
-    return *flag_lds != 0;
+    const uint32_t SEG = a.seg_bytes;
+    const uint32_t nseg = (seg_shift ? ((len - 1u) >> seg_shift) : (len - 1u) / SEG) + 1u;
+    const SegGeom geo = seg_geom((uint64_t)(uintptr_t)a.arena + off, len, nseg - 1u, nseg, SEG);
+    *c_last = size_class(geo.nl);
+    return nseg;
 }
 
 // K1: segment counts per message, the block-local exclusive prefix over the
@@ -920,28 +922,37 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
 {
     __shared__ uint32_t wsum[40];
     __shared__ uint32_t sh[4];
+    __shared__ uint32_t hist[kBuckets];
+    const bool classes = a.map_planned != 0u;  // a ragged batch is expected: size-class histogram
     if (threadIdx.x == 0) {
         sh[1] = 0;            // messages with != 1 segment
         sh[2] = 0xffffffffu;  // min segments per message
         sh[3] = 0;            // max segments per message
     }
+    if (threadIdx.x < kBuckets) {
+        hist[threadIdx.x] = 0;
+    }
     __syncthreads();
+    const int lane = threadIdx.x & 63;
     constexpr uint64_t kTile = (uint64_t)kPlanBlock * kPlanV;
     const uint64_t lo = (uint64_t)blockIdx.x * a.per_msg;
     const uint64_t hi = min(lo + a.per_msg, a.n);
     const uint32_t seg = a.seg_bytes;
     const uint32_t seg_shift = (seg & (seg - 1u)) == 0 ? (uint32_t)__builtin_ctz(seg) : 0u;
-    auto load = [&](uint64_t base, uint32_t (&L)[kPlanV]) {
+    auto load = [&](uint64_t base, uint32_t (&L)[kPlanV], uint64_t (&O)[kPlanV]) {
 #pragma unroll
         for (uint32_t v = 0; v < kPlanV; ++v) {
             const uint64_t i = base + (uint64_t)threadIdx.x * kPlanV + v;
             L[v] = i < hi ? a.lengths[i] : 0u;
+            O[v] = (classes && i < hi) ? a.offsets[i] : 0ull;
         }
     };
     uint32_t nxt[kPlanV];
+    uint64_t nxo[kPlanV];
     if (lo < hi) {
-        load(lo, nxt);
+        load(lo, nxt, nxo);
     }
+    uint32_t full = 0;  // this thread's non-last segments (all of class c_full)
     // A single-tile block (<= 4096 messages: every batch of <= 1M messages)
     // writes seg_first only if its messages differ in segment count; for a
     // uniform block consumers compute it (seg_first_g).
@@ -950,12 +961,31 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
     uint32_t ns[kPlanV], run0 = 0;
     for (uint64_t base = lo; base < hi; base += kTile) {
         uint32_t L[kPlanV];
+        uint64_t O[kPlanV];
 #pragma unroll
         for (uint32_t v = 0; v < kPlanV; ++v) {
             L[v] = nxt[v];
+            O[v] = nxo[v];
         }
         if (base + kTile < hi) {
-            load(base + kTile, nxt);  // next tile in flight during this scan
+            load(base + kTile, nxt, nxo);  // next tile in flight during this scan
+        }
+        if (classes) {
+            // class of each message's last (or only) segment, one LDS atomic
+            // per class and wave
+#pragma unroll
+            for (uint32_t v = 0; v < kPlanV; ++v) {
+                uint32_t c;
+                const uint32_t nseg = msg_segments(a, O[v], L[v], seg_shift, &c);
+                full += nseg ? nseg - 1u : 0u;
+#pragma unroll
+                for (int cc = 0; cc < kBuckets; ++cc) {
+                    const uint64_t m = __ballot(c == (uint32_t)cc);
+                    if (m && lane == 0) {
+                        atomicAdd(&hist[cc], (uint32_t)__popcll(m));
+                    }
+                }
+            }
         }
         uint32_t sum = 0;
 #pragma unroll
@@ -998,12 +1028,24 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
         mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
         non1 += (uint32_t)__shfl_xor((int)non1, o);
     }
+    if (classes) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            full += (uint32_t)__shfl_xor((int)full, o);
+        }
+    }
     if ((threadIdx.x & 63) == 0) {
         atomicMin(&sh[2], mn);
         atomicMax(&sh[3], mx);
         atomicAdd(&sh[1], non1);
+        if (full) {
+            atomicAdd(&hist[size_class(seg >> 7)], full);
+        }
     }
     __syncthreads();
+    if (classes && threadIdx.x < kBuckets) {  // read by k_plan_sort (kernel boundary)
+        a.bhist[(uint64_t)blockIdx.x * kBuckets + threadIdx.x] = hist[threadIdx.x];
+    }
     if (one_tile && sh[2] != sh[3]) {
         uint32_t run = run0;
 #pragma unroll
@@ -1020,35 +1062,6 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
         a.block_sum[a.nblocks + blockIdx.x] = sh[1];
         a.block_sum[2u * a.nblocks + blockIdx.x] = sh[2] == sh[3] ? sh[2] : 0xffffffffu;
     }
-}
-
-// Two classes per octave of the line count (1, 2, 3, 4-5, 6-7, 8-11, 12-15,
-// ..., 128-191, >= 192): lanes of a wave differ by at most 1.5x in rounds.
-// 16 buckets cover the default 16 KiB segments (<= 129 lines).
-__device__ __forceinline__ uint32_t size_class(uint32_t nl)
-{
-    nl |= 1u;
-    const uint32_t b = 31u - __clz(nl);
-    const uint32_t c = b ? 2u * b + ((nl >> (b - 1u)) & 1u) : 0u;
-    return c < kBuckets - 1 ? c : kBuckets - 1;
-}
-
-// Segments of a message (offset off, length len) and the size class of its
-// last (or only) one.  Every other segment spans exactly seg_bytes / 128
-// lines (internal boundaries are 128-byte aligned and seg_bytes is a multiple
-// of 128), so it is in class size_class(seg_bytes / 128).
-__device__ __forceinline__ uint32_t msg_segments(const BatchArgs& a, uint64_t off, uint32_t len,
-                                                 uint32_t seg_shift, uint32_t* c_last)
-{
-    *c_last = kBuckets;  // kBuckets: no segment
-    if (len == 0) {
-        return 0;
-    }
-    const uint32_t SEG = a.seg_bytes;
-    const uint32_t nseg = (seg_shift ? ((len - 1u) >> seg_shift) : (len - 1u) / SEG) + 1u;
-    const SegGeom geo = seg_geom((uint64_t)(uintptr_t)a.arena + off, len, nseg - 1u, nseg, SEG);
-    *c_last = size_class(geo.nl);
-    return nseg;
 }
 
 // Lengths and offsets of a planner tile: kPlanV messages per thread, message
@@ -1071,114 +1084,6 @@ __device__ __forceinline__ void load_tile(const BatchArgs& a, uint64_t base, uin
     }
 }
 
-// K2 (ragged batches): size-class histogram of each planner block's segments,
-// message-driven -- each thread takes whole messages, coalesced, so there is
-// no segment -> message search -- then (last block) bucket-major offsets over
-// (bucket, block) for the sort.
-__global__ __launch_bounds__(kPlanBlock) void k_plan_hist(BatchArgs a)
-{
-    __shared__ uint32_t hist[kBuckets];
-    __shared__ uint32_t flag;
-    __shared__ PlanLds pl;
-    const PlanTotals pt = plan_totals(a, &pl);
-    if (pt.identity || pt.uni) {
-        return;  // closed-form mapping; uniform across the grid: nobody takes a ticket
-    }
-    if (threadIdx.x < kBuckets) {
-        hist[threadIdx.x] = 0;
-    }
-    __syncthreads();
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t SEG = a.seg_bytes;
-    const uint32_t seg_shift = (SEG & (SEG - 1u)) == 0 ? (uint32_t)__builtin_ctz(SEG) : 0u;
-    const uint64_t lo = (uint64_t)blockIdx.x * a.per_msg;
-    const uint64_t hi = min(lo + a.per_msg, a.n);
-    uint32_t full = 0;  // this thread's non-last segments (all of class c_full)
-    constexpr uint64_t kTile = (uint64_t)kPlanBlock * kPlanV;
-    TileDesc nxt;
-    if (lo < hi) {
-        load_tile(a, lo, hi, nxt);
-    }
-    for (uint64_t base = lo; base < hi; base += kTile) {
-        const TileDesc cur = nxt;
-        if (base + kTile < hi) {
-            load_tile(a, base + kTile, hi, nxt);
-        }
-#pragma unroll
-        for (uint32_t v = 0; v < kPlanV; ++v) {
-            uint32_t c;
-            const uint32_t nseg = msg_segments(a, cur.off[v], cur.len[v], seg_shift, &c);
-            full += nseg ? nseg - 1u : 0u;
-#pragma unroll
-            for (int cc = 0; cc < kBuckets; ++cc) {  // one LDS atomic per class in the wave
-                const uint64_t m = __ballot(c == (uint32_t)cc);
-                if (m && lane == 0) {
-                    atomicAdd(&hist[cc], (uint32_t)__popcll(m));
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        full += (uint32_t)__shfl_xor((int)full, o);
-    }
-    if (lane == 0 && full) {
-        atomicAdd(&hist[size_class(SEG >> 7)], full);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int c = 0; c < kBuckets; ++c) {
-            publish(&a.bhist[(uint64_t)blockIdx.x * kBuckets + c], hist[c]);
-        }
-    }
-    if (!last_block_arrival(&a.ctrl->ticket_hist, a.nblocks, &flag)) {
-        return;
-    }
-    // last block: bucket-major exclusive offsets over (bucket, block).  Wave c
-    // scans bucket c over the blocks; thread 0 then scans the bucket totals.
-    __shared__ uint32_t btot[kBuckets];
-    __shared__ uint32_t bbase[kBuckets];
-    if (wave < kBuckets) {
-        uint32_t run = 0;
-        for (uint32_t base = 0; base < a.nblocks; base += 64) {
-            const uint32_t b = base + lane;
-            const uint32_t v = b < a.nblocks ? consume(&a.bhist[(uint64_t)b * kBuckets + wave]) : 0u;
-            uint32_t x = v;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = (uint32_t)__shfl_up((int)x, o);
-                if (lane >= o) {
-                    x += y;
-                }
-            }
-            if (b < a.nblocks) {
-                a.bhist[(uint64_t)b * kBuckets + wave] = run + x - v;
-            }
-            run += (uint32_t)__shfl((int)x, 63);
-        }
-        if (lane == 0) {
-            btot[wave] = run;
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t acc = 0;
-        for (int c = 0; c < kBuckets; ++c) {
-            bbase[c] = acc;
-            acc += btot[c];
-        }
-        // seginfo holds max_segs entries; past that k_fold searches instead
-        a.ctrl->sorted = (pt.total <= a.max_segs) ? 1u : 0u;
-        a.ctrl->ticket_hist = 0;
-    }
-    __syncthreads();
-    if (wave < kBuckets) {
-        for (uint32_t b = lane; b < a.nblocks; b += 64) {
-            a.bhist[(uint64_t)b * kBuckets + wave] += bbase[wave];
-        }
-    }
-}
-
 // K3 (ragged batches): write (message, k) of every segment into seginfo in
 // size-class order.  Each block fills its slice of every bucket (offsets from
 // K2); a message's non-last segments go to one contiguous run (same class),
@@ -1189,16 +1094,48 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_hist(BatchArgs a)
 __global__ __launch_bounds__(kPlanBlock) void k_plan_sort(BatchArgs a)
 {
     __shared__ uint32_t run[kBuckets];
+    __shared__ uint32_t part[2][kPlanBlock / kBuckets][kBuckets];
     __shared__ PlanLds pl;
     const PlanTotals pt = plan_totals(a, &pl);
-    if (pt.identity || pt.uni || !a.ctrl->sorted) {
-        return;
+    if (pt.identity || pt.uni || pt.total > a.max_segs) {
+        return;  // closed form, or more segments than seginfo holds (k_fold searches)
     }
     const int lane = threadIdx.x & 63;
-    if (threadIdx.x < kBuckets) {
-        run[threadIdx.x] = a.bhist[(uint64_t)blockIdx.x * kBuckets + threadIdx.x];
+    // This block's slice of every bucket, from k_plan's per-block histograms
+    // (bhist[block][class]): bucket-major order, so slice(c) starts at the
+    // segments of all smaller classes plus class c of the earlier blocks.
+    {
+        static_assert(kPlanBlock % kBuckets == 0, "bucket-base reduction layout");
+        constexpr uint32_t kParts = kPlanBlock / kBuckets;
+        const uint32_t c = threadIdx.x % kBuckets, pi = threadIdx.x / kBuckets;
+        uint32_t tot = 0, pre = 0;
+        for (uint32_t b = pi; b < a.nblocks; b += kParts) {
+            const uint32_t h = a.bhist[(uint64_t)b * kBuckets + c];
+            tot += h;
+            pre += b < blockIdx.x ? h : 0u;
+        }
+        part[0][pi][c] = tot;
+        part[1][pi][c] = pre;
+        __syncthreads();
+        if (threadIdx.x < kBuckets) {
+            uint32_t t = 0, q = 0;
+            for (uint32_t p = 0; p < kParts; ++p) {
+                t += part[0][p][threadIdx.x];
+                q += part[1][p][threadIdx.x];
+            }
+            part[0][0][threadIdx.x] = t;
+            part[1][0][threadIdx.x] = q;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t acc = 0;
+            for (int cc = 0; cc < kBuckets; ++cc) {
+                run[cc] = acc + part[1][0][cc];
+                acc += part[0][0][cc];
+            }
+        }
+        __syncthreads();
     }
-    __syncthreads();
     const uint32_t SEG = a.seg_bytes;
     const uint32_t seg_shift = (SEG & (SEG - 1u)) == 0 ? (uint32_t)__builtin_ctz(SEG) : 0u;
     const uint32_t c_full = size_class(SEG >> 7);
@@ -1437,7 +1374,6 @@ extern "C" int bmqcrc_launch_batch(const BatchArgs* a, void* stream, int num_cus
     if (!a->whole) {
         hipLaunchKernelGGL(k_plan, dim3(a->nblocks), dim3(kPlanBlock), 0, s, *a);
         if (a->map_planned) {
-            hipLaunchKernelGGL(k_plan_hist, dim3(a->nblocks), dim3(kPlanBlock), 0, s, *a);
             hipLaunchKernelGGL(k_plan_sort, dim3(a->nblocks), dim3(kPlanBlock), 0, s, *a);
         }
     }
