@@ -918,12 +918,13 @@ __device__ __forceinline__ uint32_t msg_segments(const BatchArgs& a, uint64_t of
 // tile's lengths are loaded before the current tile is scanned, so a block
 // pays one load latency, not one per tile.
 constexpr uint32_t kPlanV = 4;
+template <bool CLASSES>
 __global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
 {
     __shared__ uint32_t wsum[40];
     __shared__ uint32_t sh[4];
     __shared__ uint32_t hist[kBuckets];
-    const bool classes = a.map_planned != 0u;  // a ragged batch is expected: size-class histogram
+    constexpr bool classes = CLASSES;  // a ragged batch is expected: size-class histogram
     if (threadIdx.x == 0) {
         sh[1] = 0;            // messages with != 1 segment
         sh[2] = 0xffffffffu;  // min segments per message
@@ -1372,7 +1373,11 @@ extern "C" int bmqcrc_launch_batch(const BatchArgs* a, void* stream, int num_cus
         return 0;
     }
     if (!a->whole) {
-        hipLaunchKernelGGL(k_plan, dim3(a->nblocks), dim3(kPlanBlock), 0, s, *a);
+        if (a->map_planned) {
+            hipLaunchKernelGGL(k_plan<true>, dim3(a->nblocks), dim3(kPlanBlock), 0, s, *a);
+        } else {
+            hipLaunchKernelGGL(k_plan<false>, dim3(a->nblocks), dim3(kPlanBlock), 0, s, *a);
+        }
         if (a->map_planned) {
             hipLaunchKernelGGL(k_plan_sort, dim3(a->nblocks), dim3(kPlanBlock), 0, s, *a);
         }
