@@ -77,6 +77,9 @@ def parse():
     p.add_argument("--seg-bytes", type=int, default=0)
     p.add_argument("--whole-messages", action="store_true",
                    help="BMQCRC_F_WHOLE_MESSAGES: one lane per message, no planner launches")
+    p.add_argument("--msg-bytes", type=int, default=0,
+                   help="experiment: override the message size of a uniform config "
+                        "(the line is then marked as not the BASELINE workload)")
     p.add_argument("--msgs", type=int, default=0,
                    help="experiment: override the message count of a uniform config "
                         "(the line is then marked as not the BASELINE workload)")
@@ -388,10 +391,11 @@ def main():
     dev = torch.device("cuda", local)
 
     desc, gen, seed, scaling = CONFIGS[args.config]
-    if args.msgs:
-        size = UNIFORM_SIZES[args.config]  # KeyError: only uniform configs can be resized
-        gen = _uniform(args.msgs, size)
-        desc = "EXPERIMENT (not the BASELINE workload): %d msgs x %d B" % (args.msgs, size)
+    if args.msgs or args.msg_bytes:
+        size = args.msg_bytes or UNIFORM_SIZES[args.config]  # KeyError: uniform configs only
+        n_msgs = args.msgs or int(UNIFORM_SIZES[args.config] * len(gen(0, 1)[0]) // size)
+        gen = _uniform(n_msgs, size)
+        desc = "EXPERIMENT (not the BASELINE workload): %d msgs x %d B" % (n_msgs, size)
     if args.shard:
         if world > 1:
             raise SystemExit("--shard is a one-process experiment")

@@ -655,6 +655,10 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     if (!whole) {
         pw = plan_load(a);
     }
+    // x^(-8p) un-shift table -> LDS too: a per-lane index, so from constant
+    // memory it would be a vector load with a full memory latency per group
+    __shared__ uint32_t xneg8[136];
+    const uint32_t xn = threadIdx.x < 136u ? c_xneg8[threadIdx.x] : 0u;
     const uint32_t g0 = blockIdx.x * kWavesPerBlock + wave;
     const uint32_t sid = g0 * 64u + (uint32_t)lane;
     const SegDesc spec = fetch_desc(a, SegRef{sid, 0u}, sid < a.n);
@@ -664,6 +668,9 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     for (int i = 0; i < 8; ++i) {
         const uint32_t t = threadIdx.x + (uint32_t)i * (kWavesPerBlock * 64);
         *(lds_u32*)(uintptr_t)(tab_lds + 4u * t) = tw[i];
+    }
+    if (threadIdx.x < 136u) {
+        xneg8[threadIdx.x] = xn;
     }
 
     // BMQCRC_F_WHOLE_MESSAGES: segment g = message g, one segment each, no
@@ -835,7 +842,7 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         if (__ballot(padE != 0) == 0) {
             contrib = valid ? crc : 0u;
         } else if (valid) {
-            contrib = gmul(crc, c_xneg8[padE]);
+            contrib = gmul(crc, xneg8[padE]);
         }
         const uint32_t e_after = valid ? mersenne31(8ull * (mend - E)) : 0u;
         contrib = mul_xpow(contrib, e_after);
