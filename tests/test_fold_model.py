@@ -234,3 +234,43 @@ def test_first_round_equals_fold_from_zero():
             q[d] = acc
             p[(d + 31) & 31] = q[(d + 31) & 31] ^ acc
         assert first_round_pairs(m) == (q, p)
+
+
+def one_line_stop_contrib(arena, S, E, mstart, mend, first, seed):
+    """k_fold's one-line fast path: a stream of one line whose zero padding
+    after E is a multiple of 8 bytes stops its Horner after the last data word
+    instead of un-shifting by x^(-8 padE)."""
+    L0 = S & ~127
+    assert E <= L0 + 128 and (not first or E - S >= 4)
+    padE = L0 + 128 - E
+    assert padE % 8 == 0
+    stream = bytearray(128)
+    stream[S - L0:E - L0] = arena[S:E].tobytes()
+    if first:
+        for b in range(4):
+            stream[S - L0 + b] ^= ((~seed & 0xFFFFFFFF) >> (8 * b)) & 0xFF
+    words = [int(w) for w in np.frombuffer(bytes(stream), dtype="<u4")]
+    c = 0
+    for d in range(32 - padE // 4):
+        c = mul_y(c ^ words[d])
+    contrib = G.mulmod_r(c, xpow(8 * (mend - E)))
+    return contrib ^ (0xFFFFFFFF if first else 0)
+
+
+def test_one_line_stop_matches_unshift():
+    rng = np.random.default_rng(9)
+    arena = rng.integers(0, 256, size=4096, dtype=np.uint8)
+    checked = 0
+    for _ in range(400):
+        L0 = 128 * int(rng.integers(1, 30))
+        S = L0 + int(rng.integers(0, 120))
+        E = L0 + 128 - 8 * int(rng.integers(0, (L0 + 128 - S) // 8 + 1))
+        first = bool(rng.integers(0, 2))
+        if E <= S or (first and E - S < 4):
+            continue
+        seed = int(rng.integers(0, 1 << 32))
+        mend = E + 8 * int(rng.integers(0, 50))
+        assert one_line_stop_contrib(arena, S, E, S, mend, first, seed) == \
+            segment_contrib(arena, S, E, S, mend, first, seed)
+        checked += 1
+    assert checked > 100
