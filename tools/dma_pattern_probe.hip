@@ -120,7 +120,7 @@ __global__ __launch_bounds__(256, 2) void probe(const uint8_t* base, uint64_t ng
         const uint64_t my = g0 < ngroups ? (ngroups - g0 + stride - 1) / stride : 0;
         const uint64_t total = my * seglines;
         auto src_of = [&](uint64_t t) {
-            const uint64_t gi = t / seglines;
+            const uint64_t gi = seglines == 1 ? t : t / seglines;
             const uint32_t r = (uint32_t)(t - gi * seglines);
             round_src((uint64_t)(uintptr_t)base + (g0 + gi * stride) * gbytes, seglines, r, s);
         };
@@ -144,7 +144,7 @@ __global__ __launch_bounds__(256, 2) void probe(const uint8_t* base, uint64_t ng
                 src_of(t + 2);
                 dma_round(slot, s);
             }
-            if ((t + 1) % seglines == 0) {
+            if (seglines == 1 || (t + 1) % seglines == 0) {
                 acc = fake_work(acc, work);
             }
         }
@@ -167,8 +167,8 @@ int main(int argc, char** argv)
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    const uint32_t seglines_list[] = {2, 4, 16, 128};
-    const uint32_t work_list[] = {0, 400, 800};
+    const uint32_t seglines_list[] = {1, 2, 4, 16};
+    const uint32_t work_list[] = {0, 200, 400, 800};
     for (uint32_t sl : seglines_list) {
         for (uint32_t work : work_list) {
             for (uint32_t mode = 0; mode < 2; ++mode) {
