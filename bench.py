@@ -263,7 +263,8 @@ def protocol(args):
         bad[int(app_off[i]) + 17] ^= 0x5A
     found = storage.verify_partition(journal, bad)
     jrec0 = journal.size - n * storage.JOURNAL_RECORD_SIZE
-    exp_off = [jrec0 + i * storage.JOURNAL_RECORD_SIZE for i in planted]
+    # alarms come in the reference's (backward) journal order
+    exp_off = [jrec0 + i * storage.JOURNAL_RECORD_SIZE for i in reversed(planted)]
     parity = {"n_bad": res["n_bad"], "planted": len(planted),
               "found_exact": found["bad_record_offsets"].tolist() == exp_off}
     line("recovery_verify", "mqbs::FileStore::recoverMessages CRC check "

@@ -93,9 +93,13 @@ lib.bmqcrc_put_event_fill_crcs.argtypes = [_vp, _u64, _popts]
 lib.bmqcrc_put_event_verify.restype = _int
 lib.bmqcrc_put_event_verify.argtypes = [_vp, _u64, _pu64, _pu64, _vp, _u64, _popts]
 lib.bmqcrc_journal_scan.restype = _i64
-lib.bmqcrc_journal_scan.argtypes = [_vp, _u64, _vp, _u64, _vp, _vp, _vp, _vp, _u64]
+lib.bmqcrc_journal_scan.argtypes = [_vp, _u64, _vp, _u64, _vp, _pint, _pu64, _vp, _vp, _vp, _vp,
+                                    _u64]
+lib.bmqcrc_journal_bounds.restype = _int
+lib.bmqcrc_journal_bounds.argtypes = [_vp, _u64, _pu64, _pu64]
 lib.bmqcrc_recover_verify.restype = _int
-lib.bmqcrc_recover_verify.argtypes = [_vp, _u64, _vp, _u64, _pu64, _pu64, _vp, _u64, _popts]
+lib.bmqcrc_recover_verify.argtypes = [_vp, _u64, _vp, _u64, _vp, _pint, _pu64, _pu64, _pu64, _vp,
+                                      _u64, _popts]
 lib.bmqcrc_csl_scan.restype = _i64
 lib.bmqcrc_csl_scan.argtypes = [_vp, _u64, _vp, _vp, _vp, _vp, _u64, _pint, _pu64]
 lib.bmqcrc_csl_validate.restype = _int

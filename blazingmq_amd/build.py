@@ -44,10 +44,11 @@ def build_consts():
         _run([sys.executable, gen, out])
 
 
-def build_product(force=False):
+def build_product(force=False, defines=(), target_name="libbmqcrc.so"):
+    """defines: extra -D flags for same-box A/B variants (tools/build_variant.sh)."""
     os.makedirs(LIB, exist_ok=True)
     build_consts()
-    target = os.path.join(LIB, "libbmqcrc.so")
+    target = os.path.join(LIB, target_name)
     srcs = [os.path.join(CSRC, s) for s in PRODUCT_SOURCES]
     deps = srcs + [os.path.join(CSRC, d) for d in PRODUCT_DEPS] + [
         os.path.join(ROOT, "include", "bmqcrc.h"), os.path.join(ROOT, "include", "bmqp_crc32c.h"),
@@ -57,7 +58,7 @@ def build_product(force=False):
         for s in srcs:
             o = os.path.join(LIB, os.path.basename(s) + ".o")
             cmd = [HIPCC, "-O3", "-fPIC", "-std=c++17", "-Wall", "-I" + os.path.join(ROOT, "include"),
-                   "-c", s, "-o", o]
+                   *defines, "-c", s, "-o", o]
             if s.endswith(".hip"):
                 cmd[1:1] = ["-x", "hip", "--offload-arch=" + ARCH, "-munsafe-fp-atomics"]
             _run(cmd)
@@ -67,10 +68,12 @@ def build_product(force=False):
         for o in objs:
             os.remove(o)
         for leftover in os.listdir(LIB):  # hipcc offload-bundling intermediates
-            if leftover.startswith("libbmqcrc.so."):
+            if leftover.startswith(target_name + "."):
                 os.remove(os.path.join(LIB, leftover))
     selftest = os.path.join(ROOT, "tests", "cpp", "bin", "bmqp_selftest")
     st_src = os.path.join(ROOT, "tests", "cpp", "bmqp_crc32c_selftest.cpp")
+    if target_name != "libbmqcrc.so":
+        return target
     if os.path.exists(st_src) and (force or _stale(selftest, [st_src, target])):
         os.makedirs(os.path.dirname(selftest), exist_ok=True)
         _run(["g++", "-O2", "-std=c++17", "-I" + os.path.join(ROOT, "include"), st_src,

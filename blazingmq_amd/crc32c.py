@@ -143,13 +143,14 @@ def _batch_torch(torch, arena, offsets, lengths, seeds, out, seg_bytes, stream, 
             raise TypeError("%s must be a contiguous %s tensor on %s" % (name, dt, dev))
     if lengths.numel() != n:
         raise ValueError("offsets/lengths size mismatch")
-    if seeds is not None and (seeds.device != dev or seeds.dtype != torch.int32
-                              or seeds.numel() != n):
-        raise TypeError("seeds must be an int32 tensor of n elements on %s" % dev)
+    if seeds is not None and not _is_vec(torch, seeds, dev, torch.int32, n):
+        raise TypeError("seeds must be a contiguous int32 tensor of %d elements on %s" % (n, dev))
     if arena.dtype != torch.uint8 or not arena.is_contiguous():
         raise TypeError("arena must be a contiguous uint8 tensor")
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=dev)
+    elif not _is_vec(torch, out, dev, torch.int32, n):
+        raise TypeError("out must be a contiguous int32 tensor of %d elements on %s" % (n, dev))
     if stream is None:
         stream = torch.cuda.current_stream(dev)
     flags = _native.BMQCRC_F_DEVICE_PTRS | (0 if sync else _native.BMQCRC_F_ASYNC)
@@ -165,6 +166,19 @@ def _batch_torch(torch, arena, offsets, lengths, seeds, out, seg_bytes, stream, 
     return out
 
 
+def _is_vec(torch, t, dev, dtype, n):
+    """A contiguous 1-D-sized tensor of n elements of dtype on dev."""
+    return (isinstance(t, torch.Tensor) and t.device == dev and t.dtype == dtype
+            and t.is_contiguous() and t.numel() == n)
+
+
+def _check_host_out(out, n):
+    if not (isinstance(out, np.ndarray) and out.dtype == np.uint32 and out.size == n
+            and out.flags.c_contiguous and out.flags.writeable):
+        raise TypeError("out must be a writeable C-contiguous uint32 ndarray of %d elements" % n)
+    return out
+
+
 def _batch_host(arena, offsets, lengths, seeds, out, seg_bytes, device, whole_messages=False):
     a = np.frombuffer(bytes(arena), dtype=np.uint8) if isinstance(
         arena, (bytes, bytearray, memoryview)) else np.ascontiguousarray(arena).view(np.uint8)
@@ -173,7 +187,9 @@ def _batch_host(arena, offsets, lengths, seeds, out, seg_bytes, device, whole_me
     if off.shape != ln.shape:
         raise ValueError("offsets/lengths size mismatch")
     sd = None if seeds is None else np.ascontiguousarray(seeds, dtype=np.uint32)
-    res = np.empty(off.size, dtype=np.uint32) if out is None else out
+    if sd is not None and sd.shape != off.shape:
+        raise ValueError("seeds must have one entry per message")
+    res = np.empty(off.size, dtype=np.uint32) if out is None else _check_host_out(out, off.size)
     o = _native.make_opts(device=-1 if device is None else device, seg_bytes=seg_bytes,
                           flags=_native.BMQCRC_F_WHOLE_MESSAGES if whole_messages else 0)
     _native.check(_native.lib.bmqcrc_crc32c_batch(
@@ -317,8 +333,15 @@ def calculate_batch_ptr(arena_ptr, arena_bytes, offsets, lengths, seeds=None, ou
     import torch
     dev = offsets.device
     n = offsets.numel()
+    if not _is_vec(torch, offsets, dev, torch.int64, n) or \
+            not _is_vec(torch, lengths, dev, torch.int32, n):
+        raise TypeError("offsets/lengths must be contiguous int64/int32 tensors of n elements")
+    if seeds is not None and not _is_vec(torch, seeds, dev, torch.int32, n):
+        raise TypeError("seeds must be a contiguous int32 tensor of %d elements on %s" % (n, dev))
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=dev)
+    elif not _is_vec(torch, out, dev, torch.int32, n):
+        raise TypeError("out must be a contiguous int32 tensor of %d elements on %s" % (n, dev))
     if stream is None:
         stream = torch.cuda.current_stream(dev)
     flags = _native.BMQCRC_F_DEVICE_PTRS | (0 if sync else _native.BMQCRC_F_ASYNC)

@@ -48,6 +48,27 @@ int fail(int rc, const std::string& msg)
         }                                                                                   \
     } while (0)
 
+// Restores the calling thread's current HIP device on scope exit: the library
+// selects the device a call targets, and a drop-in must not retarget the
+// caller's later HIP/torch work on that thread.
+struct DeviceGuard {
+    int prev = -1;
+    DeviceGuard()
+    {
+        if (hipGetDevice(&prev) != hipSuccess) {
+            prev = -1;
+        }
+    }
+    ~DeviceGuard()
+    {
+        if (prev >= 0) {
+            (void)hipSetDevice(prev);
+        }
+    }
+    DeviceGuard(const DeviceGuard&) = delete;
+    DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+
 struct DevBuf {
     void* p = nullptr;
     uint64_t bytes = 0;
@@ -304,18 +325,14 @@ int run_batch(Ctx& c, uint32_t flags, uint32_t seg, const void* arena, uint64_t 
     a.n = n;
     auto_shape(n, arena_bytes, c.st->num_cus, &seg, &a.blocks_per_cu);
     a.seg_bytes = seg;
-    static const uint32_t tune = [] {
-        const char* e = getenv("BMQCRC_TUNE");  // experiment knob, see BatchArgs::tune
-        return e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
-    }();
-    a.tune = tune;
+    a.tune = kTuneBits;
     int rc;
     if (flags & BMQCRC_F_WHOLE_MESSAGES) {
         a.whole = 1;  // identity map over messages: no planner workspace
         a.max_segs = n;
     } else if ((rc = plan_ws(w, n, arena_bytes, seg, &a))) {
         return rc;
-    } else if (!(tune & 16u) &&
+    } else if (!(kTuneBits & 16u) &&
                __atomic_load_n(w->hint_host, __ATOMIC_RELAXED) == kHintClosed) {
         a.map_planned = 0;  // last batch was closed-form: predict this one is too
     }
@@ -431,7 +448,7 @@ int check_ranges(const uint64_t* offsets, const uint32_t* lengths, uint64_t n,
 int verify_locked(Ctx& c, Workspace* w, const bmqcrc_opts& o, uint32_t seg, bool arena_staged,
                   const void* arena, uint64_t arena_bytes, const uint64_t* offsets,
                   const uint32_t* lengths, const uint32_t* expected, uint64_t n, uint64_t* n_bad,
-                  uint64_t* bad_idx, uint64_t bad_cap);
+                  uint64_t* bad_idx, uint64_t bad_cap, uint64_t* n_written);
 
 }  // namespace
 
@@ -472,6 +489,7 @@ int bmqcrc_crc32c_batch(const void* arena, uint64_t arena_bytes, const uint64_t*
                         uint64_t n, const bmqcrc_opts* opts)
 {
     t_err.clear();
+    DeviceGuard keep_device;
     if (n == 0) {
         return 0;
     }
@@ -500,6 +518,7 @@ int bmqcrc_crc32c_verify(const void* arena, uint64_t arena_bytes, const uint64_t
                          const bmqcrc_opts* opts)
 {
     t_err.clear();
+    DeviceGuard keep_device;
     if (!n_bad) {
         return fail(BMQCRC_EINVAL, "n_bad is required");
     }
@@ -530,7 +549,7 @@ int bmqcrc_crc32c_verify(const void* arena, uint64_t arena_bytes, const uint64_t
     Workspace* w = c.w;
     std::lock_guard<std::mutex> g(w->mu);
     return verify_locked(c, w, o, seg, false, arena, arena_bytes, offsets, lengths, expected, n,
-                         n_bad, bad_idx, bad_cap);
+                         n_bad, bad_idx, bad_cap, nullptr);
 }
 
 }  // extern "C"
@@ -543,11 +562,16 @@ namespace {
 int verify_locked(Ctx& c, Workspace* w, const bmqcrc_opts& o, uint32_t seg, bool arena_staged,
                   const void* arena, uint64_t arena_bytes, const uint64_t* offsets,
                   const uint32_t* lengths, const uint32_t* expected, uint64_t n, uint64_t* n_bad,
-                  uint64_t* bad_idx, uint64_t bad_cap)
+                  uint64_t* bad_idx, uint64_t bad_cap, uint64_t* n_written)
 {
     int rc;
     const bool dev_ptrs = (o.flags & BMQCRC_F_DEVICE_PTRS) != 0;
-    const uint32_t cap = (uint32_t)std::min<uint64_t>(bad_cap, 1u << 24);
+    // n < 2^32, so every mismatch index fits the device list: exactly
+    // min(n_bad, bad_cap) indices are written.
+    const uint32_t cap = (uint32_t)std::min<uint64_t>(bad_cap, n);
+    if (n_written) {
+        *n_written = 0;
+    }
     if ((rc = w->out.ensure(4 * n)) || (rc = w->vcount.ensure(4)) ||
         (rc = w->vidx.ensure(4ull * std::max<uint32_t>(cap, 1)))) {
         return rc;
@@ -619,6 +643,9 @@ int verify_locked(Ctx& c, Workspace* w, const bmqcrc_opts& o, uint32_t seg, bool
             bad_idx[k] = idx[k];
         }
     }
+    if (n_written) {
+        *n_written = take;
+    }
     return 0;
 }
 
@@ -628,9 +655,14 @@ int verify_locked(Ctx& c, Workspace* w, const bmqcrc_opts& o, uint32_t seg, bool
 int bmqcrc_verify_host_overlapped(const void* arena, uint64_t arena_bytes,
                                   bmqcrc_prepare_fn prepare, void* pctx, uint64_t* n_bad,
                                   std::vector<uint64_t>* bad, uint64_t bad_cap,
-                                  const bmqcrc_opts* opts, std::vector<uint32_t>* crcs)
+                                  const bmqcrc_opts* opts, std::vector<uint32_t>* crcs,
+                                  uint64_t* n_written)
 {
+    if (n_written) {
+        *n_written = 0;
+    }
     t_err.clear();
+    DeviceGuard keep_device;
     if (!prepare || (!crcs && (!n_bad || !bad)) || (!arena && arena_bytes)) {
         return fail(BMQCRC_EINVAL, "null pointer argument");
     }
@@ -639,19 +671,20 @@ int bmqcrc_verify_host_overlapped(const void* arena, uint64_t arena_bytes,
     }
     bmqcrc_opts o;
     uint32_t seg;
-    int dev, rc;
-    if ((rc = parse_opts(opts, &o, &seg, &dev))) {
+    int dev = 0, rc;
+    const uint64_t* off = nullptr;
+    const uint32_t* len = nullptr;
+    const uint32_t* exp = nullptr;
+    uint64_t n = 0;
+    rc = parse_opts(opts, &o, &seg, &dev);
+    if (rc && rc != BMQCRC_ENODEV) {
         return rc;
     }
     if (o.flags & (BMQCRC_F_DEVICE_PTRS | BMQCRC_F_ASYNC)) {
         return fail(BMQCRC_EINVAL, "overlapped verify takes host buffers, synchronously");
     }
-    const uint64_t* off = nullptr;
-    const uint32_t* len = nullptr;
-    const uint32_t* exp = nullptr;
-    uint64_t n = 0;
     Ctx c;
-    if ((rc = open_ctx(dev, o.stream, &c))) {
+    if (rc || (rc = open_ctx(dev, o.stream, &c))) {
         // no usable device: a malformed input is still reported first
         const std::string why = t_err;
         const int prc = prepare(pctx, &off, &len, &exp, &n);
@@ -710,7 +743,7 @@ int bmqcrc_verify_host_overlapped(const void* arena, uint64_t arena_bytes,
     }
     bad->assign(std::min<uint64_t>(bad_cap, n), 0);
     return verify_locked(c, w, o, seg, true, arena, arena_bytes, off, len, exp, n, n_bad,
-                         bad->data(), bad->size());
+                         bad->data(), bad->size(), n_written);
 }
 
 extern "C" {
@@ -721,6 +754,7 @@ int bmqcrc_crc32c_blobs(const void* arena, uint64_t arena_bytes, const uint64_t*
                         uint64_t n, const bmqcrc_opts* opts)
 {
     t_err.clear();
+    DeviceGuard keep_device;
     if (n == 0) {
         return 0;
     }
@@ -885,6 +919,7 @@ int bmqcrc_reserve(int device, void* stream, uint64_t n_msgs, uint64_t arena_byt
                    uint32_t seg_bytes)
 {
     t_err.clear();
+    DeviceGuard keep_device;
     int dev, rc;
     if ((rc = check_seg(&seg_bytes)) || (rc = resolve_device(device, &dev))) {
         return rc;
@@ -906,6 +941,7 @@ int bmqcrc_fill_synthetic(void* dev_dst, uint64_t nbytes, uint64_t seed, uint64_
                           const bmqcrc_opts* opts)
 {
     t_err.clear();
+    DeviceGuard keep_device;
     int dev, rc;
     if ((rc = resolve_device(opts ? opts->device : -1, &dev))) {
         return rc;
@@ -931,6 +967,7 @@ int bmqcrc_fill_synthetic(void* dev_dst, uint64_t nbytes, uint64_t seed, uint64_
 int bmqcrc_kernel_timing(int device, void* stream, double* total_ms, uint32_t* count)
 {
     t_err.clear();
+    DeviceGuard keep_device;
     int dev, rc;
     if ((rc = resolve_device(device, &dev))) {
         return rc;
@@ -961,6 +998,7 @@ int bmqcrc_kernel_timing(int device, void* stream, double* total_ms, uint32_t* c
 int bmqcrc_host_register(void* host, uint64_t bytes, int device, void** dev_ptr)
 {
     t_err.clear();
+    DeviceGuard keep_device;
     if (!host || !bytes || !dev_ptr) {
         return fail(BMQCRC_EINVAL, "host, bytes and dev_ptr are required");
     }
@@ -1006,7 +1044,7 @@ const char* bmqcrc_last_error(void)
 
 uint32_t bmqcrc_version(void)
 {
-    return (1u << 16) | 0u;
+    return (2u << 16) | 0u;
 }
 
 }  // extern "C"

@@ -19,6 +19,15 @@ constexpr int kPlanMaxBlocks = 256;  // planner grids: contiguous message ranges
 
 constexpr int kBuckets = 16;            // segment size classes: floor(log2(lines))
 
+// Experiment knobs for same-box A/B builds (tools/build_variant.sh
+// -DBMQCRC_TUNE_BITS=...); the product is built with 0.  bit0 disables the
+// non-temporal LDS-DMA loads, bit1 forces a 1-block/CU k_fold grid, bit3
+// forces 2, bit4 always builds the size-class map (no shape prediction).
+#ifndef BMQCRC_TUNE_BITS
+#define BMQCRC_TUNE_BITS 0u
+#endif
+constexpr uint32_t kTuneBits = BMQCRC_TUNE_BITS;
+
 struct BatchArgs {
     const uint8_t* arena;      // device
     const uint64_t* offsets;   // device, n
@@ -38,9 +47,7 @@ struct BatchArgs {
     uint32_t nblocks;          // planner blocks (<= kPlanMaxBlocks)
     uint32_t whole;            // 1: BMQCRC_F_WHOLE_MESSAGES (one segment per message, no planner)
     uint32_t blocks_per_cu;    // k_fold grid: 1 (large messages) or 2 blocks per CU
-    uint32_t tune;             // experiment knobs (BMQCRC_TUNE env): bit0 disables nt LDS-DMA
-                               // loads, bit1 forces a 1-block/CU grid, bit3 forces 2, bit4
-                               // always builds the histogram and launches k_plan_sort
+    uint32_t tune;             // experiment knobs, fixed at build time (BMQCRC_TUNE_BITS below)
     uint32_t map_planned;      // 1: k_plan builds the size-class histogram and k_plan_sort
                                //    runs before k_fold; 0: skipped (the previous batch on this
                                //    workspace was closed-form) and a ragged batch maps segments
@@ -79,17 +86,17 @@ extern "C" __attribute__((visibility("hidden"))) int bmqcrc_launch_compare_order
 // arrays of n messages, or a BMQCRC_E* code with the error already set.
 typedef int (*bmqcrc_prepare_fn)(void* ctx, const uint64_t** offsets, const uint32_t** lengths,
                                  const uint32_t** expected, uint64_t* n);
-// `bad` receives the lowest min(bad_cap, n) mismatching indices' slots (the
-// first min(*n_bad, size) are valid), like bmqcrc_crc32c_verify.  With `crcs`
-// non-null the call computes instead of verifying: crcs = the n CRCs
-// (expected, n_bad and bad are then unused).  C++ only.
+// `bad` receives the lowest min(*n_bad, bad_cap) mismatching indices, like
+// bmqcrc_crc32c_verify; *n_written (if non-null) = how many were written.
+// With `crcs` non-null the call computes instead of verifying: crcs = the n
+// CRCs (expected, n_bad and bad are then unused).  C++ only.
 #ifdef __cplusplus
 #include <vector>
 struct bmqcrc_opts;
 __attribute__((visibility("hidden"))) int bmqcrc_verify_host_overlapped(
     const void* arena, uint64_t arena_bytes, bmqcrc_prepare_fn prepare, void* pctx,
     uint64_t* n_bad, std::vector<uint64_t>* bad, uint64_t bad_cap, const bmqcrc_opts* opts,
-    std::vector<uint32_t>* crcs = nullptr);
+    std::vector<uint32_t>* crcs = nullptr, uint64_t* n_written = nullptr);
 #endif
 // Thread-local error message shared by every C-ABI source (bmqcrc_last_error).
 extern "C" __attribute__((visibility("hidden"))) int bmqcrc_set_error(int rc, const char* msg);

@@ -9,8 +9,10 @@
 #include <string.h>
 
 #include <algorithm>
-#include <string>
 #include <functional>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/bmqcrc.h"
@@ -109,16 +111,31 @@ int walk_put_event(const uint8_t* ev, uint64_t len, Ranges* r)
 // Partition files (mqbs_filestoreprotocol.h).  FileHeader (:306): "!bmq"
 // "BMQ!", u8 PV(2)|HeaderWords(6), u8 Bitness(1)|FileType(7).  Journal
 // (:483): JournalFileHeader u8 headerWords, u8 recordWords (15), then 60-byte
-// records; MessageRecord (:1125): type nibble in byte 0, messageOffsetDwords
-// BE @32, CRC32-C BE @52, magic "*rEc" BE @56.  DATA record (:703):
-// DataHeader BE u32 HW(3)|messageWords(29), BE u32 optionsWords(24)|flags(8),
-// options, application data, 1..8 padding bytes equal to the count.
+// records.  Every record starts with a RecordHeader (:1014): BE u16
+// type(4)|flags(12), BE u16 + BE u32 sequence number (48 bits), BE u32
+// primary lease id, BE u64 timestamp; and ends with the magic "*rEc" @56.
+// Record bodies (byte offsets in the 60-byte record):
+//   MessageRecord   (:1125) queueKey[5] @22, messageOffsetDwords @32,
+//                           GUID[16] @36, CRC32-C @52
+//   ConfirmRecord   (:1339) queueKey @22, appKey @27, GUID @32
+//   DeletionRecord  (:1518) queueKey @23, GUID @28
+//   QueueOpRecord   (:1694) queueKey @22, appKey @27, BE i32 QueueOpType @32
+//   JournalOpRecord (:1953) syncPointType u8 @23, BE i32 JournalOpType @24,
+//                           sequence number @28/@32, primary lease id @40,
+//                           dataFileOffsetDwords @44
+// DATA record (:703): DataHeader BE u32 HW(3)|messageWords(29), BE u32
+// optionsWords(24)|flags(8), options, application data, 1..8 padding bytes
+// equal to the count.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kMagic1 = 0x21626D71u;  // "!bmq"
 constexpr uint32_t kMagic2 = 0x424D5121u;  // "BMQ!"
 constexpr uint32_t kRecordMagic = 0x2A724563u;
 constexpr uint32_t kFileData = 1, kFileJournal = 2;
-constexpr uint32_t kRecMessage = 1;
+constexpr uint32_t kRecUndefined = 0, kRecMessage = 1, kRecConfirm = 2, kRecDeletion = 3,
+                   kRecQueueOp = 4, kRecJournalOp = 5;                 // RecordType (:953)
+constexpr int32_t kOpUndefined = 0, kOpPurge = 1, kOpCreation = 2, kOpDeletion = 3,
+                  kOpAddition = 4;                                     // QueueOpType (:1630)
+constexpr int32_t kJournalOpSyncPoint = 2;                             // JournalOpType (:1841)
 constexpr uint64_t kJournalRecord = 60;
 
 int file_header_size(const uint8_t* a, uint64_t len, uint32_t want_type, uint64_t* size)
@@ -136,7 +153,121 @@ int file_header_size(const uint8_t* a, uint64_t len, uint32_t want_type, uint64_
     return 0;
 }
 
-int walk_partition(const uint8_t* j, uint64_t jlen, const uint8_t* d, uint64_t dlen, Ranges* r)
+struct RecHeader {
+    uint32_t type;
+    uint32_t lease;
+    uint64_t seq;
+};
+
+inline RecHeader rec_header(const uint8_t* r)
+{
+    RecHeader h;
+    h.type = r[0] >> 4;
+    h.seq = ((uint64_t)(((uint32_t)r[2] << 8) | r[3]) << 32) | be32(r + 4);
+    h.lease = be32(r + 8);
+    return h;
+}
+
+// mqbu::StorageKey (5 bytes) as an integer; the null key is 0.
+inline uint64_t key5(const uint8_t* p)
+{
+    return ((uint64_t)p[0] << 32) | ((uint64_t)p[1] << 24) | ((uint64_t)p[2] << 16) |
+           ((uint64_t)p[3] << 8) | p[4];
+}
+
+struct Guid {
+    uint64_t hi, lo;
+    bool operator==(const Guid& o) const { return hi == o.hi && lo == o.lo; }
+    bool unset() const { return hi == 0 && lo == 0; }  // bmqt::MessageGUID::isUnset
+};
+
+inline Guid guid_at(const uint8_t* p)
+{
+    Guid g{0, 0};
+    for (int i = 0; i < 8; ++i) {
+        g.hi = (g.hi << 8) | p[i];
+        g.lo = (g.lo << 8) | p[8 + i];
+    }
+    return g;
+}
+
+struct GuidHash {
+    size_t operator()(const Guid& g) const
+    {
+        return (size_t)(g.hi * 0x9E3779B97F4A7C15ull ^ (g.lo + 0x632BE59BD9B4E019ull));
+    }
+};
+
+// FileStoreProtocolUtil::lastJournalSyncPoint (mqbs_filestoreprotocolutil.cpp:165-228):
+// scan backwards for the last well-formed SYNCPOINT JournalOp record; 0 = none.
+uint64_t last_sync_point_of(const uint8_t* j, uint64_t jlen, uint64_t start)
+{
+    if (jlen <= start) {
+        return 0;
+    }
+    const uint64_t nrec = (jlen - start) / kJournalRecord;
+    for (uint64_t i = 1; i <= nrec; ++i) {
+        const uint64_t pos = start + (nrec - i) * kJournalRecord;
+        const uint8_t* r = j + pos;
+        const RecHeader h = rec_header(r);
+        if (h.type != kRecJournalOp || (int32_t)be32(r + 24) != kJournalOpSyncPoint ||
+            h.lease == 0 || h.seq == 0 || be32(r + 56) != kRecordMagic) {
+            continue;
+        }
+        return pos;
+    }
+    return 0;
+}
+
+// FileStoreProtocolUtil::lastJournalRecord (:230-289): from the last sync
+// point, forward until a record with an undefined type or a bad magic; the
+// record before it is the last one.  0 = the journal holds no record.
+uint64_t last_record(const uint8_t* j, uint64_t jlen, uint64_t start, uint64_t lsp)
+{
+    if (jlen <= start) {
+        return 0;
+    }
+    uint64_t cur = lsp ? lsp + kJournalRecord : start;
+    uint64_t prev = lsp;
+    while (cur + kJournalRecord <= jlen) {
+        const uint8_t* r = j + cur;
+        if ((r[0] >> 4) == kRecUndefined || be32(r + kJournalRecord - 4) != kRecordMagic) {
+            return prev;
+        }
+        prev = cur;
+        cur += kJournalRecord;
+    }
+    return prev;
+}
+
+// What FileStore::recoverMessages knows about the partition's queues: with
+// CSL the cluster state's queue keys, without it the keys of the journal's
+// QueueOp CREATION records (its first pass).
+struct QueueView {
+    bool with_csl = false;
+    std::unordered_set<uint64_t> keys;  // queueKeyInfoMap
+};
+
+struct RecoveryResult {
+    int rc = BMQCRC_RECOVERY_SUCCESS;
+    uint64_t error_record = 0;  // journal offset of the record that failed recovery
+};
+
+// mqbs::FileStore::recoverMessages (mqbs_filestore.cpp:1045-2666) reduced to
+// the decisions that select which MESSAGE records get their payload CRC'd
+// (:2603-2624) and the record checks that abort recovery on the way.  Both
+// passes iterate the journal backwards from its last record
+// (JournalFileIterator in reverse mode, mqbs_journalfileiterator.cpp:38-281),
+// stopping at the first record with an undefined type, a zero lease id or
+// sequence number, or a bad magic.  The write head is the last record's PSN
+// (the FSM workflow, mqbs_filestore.cpp:497-517).  Ranges come out in that
+// backward order, which is the order the reference raises its alarms in.
+//
+// Not restated: the QLIST file (the partition is read qlist-unaware), the
+// in-memory record map, purges of one appKey (they do not skip the message's
+// CRC) and the legacy multi-node truncation to the last sync point.
+int walk_recovery(const uint8_t* j, uint64_t jlen, const uint8_t* d, uint64_t dlen,
+                  QueueView* qv, Ranges* r, RecoveryResult* res)
 {
     uint64_t fh = 0, dfh = 0;
     int rc;
@@ -147,6 +278,9 @@ int walk_partition(const uint8_t* j, uint64_t jlen, const uint8_t* d, uint64_t d
     if (fh + 2 > jlen) {
         return bad_format("truncated JournalFileHeader", fh);
     }
+    if (j[fh] == 0) {  // JournalFileIterator::reset rc_CORRUPT_JOURNAL_HEADER
+        return bad_format("JournalFileHeader headerWords is zero", fh);
+    }
     if ((uint64_t)j[fh + 1] * 4 != kJournalRecord) {
         return bad_format("journal recordWords != 15", fh + 1);
     }
@@ -154,44 +288,212 @@ int walk_partition(const uint8_t* j, uint64_t jlen, const uint8_t* d, uint64_t d
     if (start > jlen) {
         return bad_format("JournalFileHeader headerWords out of range", fh);
     }
-    const uint64_t nrec = (jlen - start) / kJournalRecord;
-    for (uint64_t i = 0; i < nrec; ++i) {
-        const uint64_t ro = start + i * kJournalRecord;
-        const uint8_t* rec = j + ro;
-        if (be32(rec + 56) != kRecordMagic) {
-            // a pre-allocated journal is zero past the last record
-            for (uint64_t b = ro; b < start + nrec * kJournalRecord; ++b) {
-                if (j[b]) {
-                    return bad_format("journal record with a bad magic", ro);
-                }
-            }
+    const uint64_t last = last_record(j, jlen, start, last_sync_point_of(j, jlen, start));
+    if (last == 0) {
+        return 0;  // no records: nothing to recover
+    }
+    // Records of the backward iteration: last, last - 60, ..., start.
+    auto valid = [&](uint64_t pos) {
+        const uint8_t* rec = j + pos;
+        const RecHeader h = rec_header(rec);
+        return h.type != kRecUndefined && h.lease != 0 && h.seq != 0 &&
+               be32(rec + kJournalRecord - 4) == kRecordMagic;
+    };
+    auto fail_at = [&](int code, uint64_t pos) {
+        res->rc = code;
+        res->error_record = pos;
+        return 0;
+    };
+    auto live = [&](uint64_t key) { return qv->keys.count(key) != 0; };
+
+    // ---- first pass (:1120-1453): deleted queues, queues alive without CSL,
+    // the first sync point's offset.
+    std::unordered_map<uint64_t, uint64_t> deleted_queue;  // queueKey -> DELETION offset
+    std::unordered_map<uint64_t, uint64_t> deleted_app;    // appKey -> DELETION offset
+    uint64_t first_sync = 0;
+    for (uint64_t pos = last + kJournalRecord; pos >= start + kJournalRecord;) {
+        pos -= kJournalRecord;
+        if (!valid(pos)) {
             break;
         }
-        if ((rec[0] >> 4) != kRecMessage) {
+        const uint8_t* rec = j + pos;
+        const uint32_t type = rec[0] >> 4;
+        if (type == kRecJournalOp) {
+            first_sync = pos;
             continue;
         }
-        const uint64_t o = (uint64_t)be32(rec + 32) * 8;
-        if (o + 8 > dlen) {
-            return bad_format("DATA record offset beyond the DATA file", ro);
+        if (type != kRecQueueOp) {
+            continue;
         }
-        const uint32_t w0 = be32(d + o), w1 = be32(d + o + 4);
-        const uint64_t hs = (uint64_t)(w0 >> 29) * 4;
-        const uint64_t total = (uint64_t)(w0 & 0x1FFFFFFFu) * 4;
-        const uint64_t opt = (uint64_t)(w1 >> 8) * 4;
-        if (hs == 0 || total == 0) {
-            return bad_format("DATA record with zero headerWords/messageWords", o);
+        const int32_t op = (int32_t)be32(rec + 32);
+        const uint64_t qkey = key5(rec + 22), akey = key5(rec + 27);
+        if (op == kOpUndefined) {
+            return fail_at(BMQCRC_RECOVERY_INVALID_QUEUE_OP_RECORD, pos);
         }
-        if (hs + opt >= total) {
-            return bad_format("DATA record header/options exceed messageWords", o);
+        if (qkey == 0) {
+            return fail_at(BMQCRC_RECOVERY_NULL_QUEUE_KEY, pos);
         }
-        if (o + total > dlen) {
-            return bad_format("DATA record extends beyond the DATA file", o);
+        if (op == kOpDeletion) {
+            if (qv->with_csl && akey == 0 && live(qkey)) {
+                return fail_at(BMQCRC_RECOVERY_INVALID_DELETION_RECORD, pos);
+            }
+            // the last DELETION of a key (the first one met backwards) counts
+            (akey == 0 ? deleted_queue : deleted_app).emplace(akey == 0 ? qkey : akey, pos);
+        } else if (op == kOpPurge) {
+            continue;
+        } else if (op == kOpAddition || op == kOpCreation) {
+            if (deleted_queue.count(qkey)) {
+                continue;
+            }
+            if (qv->with_csl) {
+                if (!live(qkey)) {
+                    return fail_at(BMQCRC_RECOVERY_INVALID_QUEUE_KEY, pos);
+                }
+            } else if (op == kOpAddition) {
+                if (live(qkey)) {  // a CREATION met earlier backwards: two live queues
+                    return fail_at(BMQCRC_RECOVERY_DUPLICATE_QUEUE_KEY, pos);
+                }
+            } else if (!qv->keys.insert(qkey).second) {
+                return fail_at(BMQCRC_RECOVERY_DUPLICATE_QUEUE_KEY, pos);
+            }
         }
-        const uint32_t pad = d[o + total - 1];
-        if (pad < 1 || pad > 8 || total < hs + opt + pad) {
-            return bad_format("DATA record with invalid padding", o + total - 1);
+        // any other QueueOpType: alarmed and skipped (:1443-1451)
+    }
+
+    // ---- second pass (:1490-2646)
+    std::unordered_set<Guid, GuidHash> deleted_guids;
+    std::unordered_set<uint64_t> purged_queues;
+    const RecHeader head = rec_header(j + last);
+    uint32_t lease = head.lease;
+    uint64_t seq = head.seq + 1;
+    auto before_queue_deletion = [&](uint64_t qkey, uint64_t pos) {
+        auto it = deleted_queue.find(qkey);
+        return it != deleted_queue.end() && pos < it->second;
+    };
+    for (uint64_t pos = last + kJournalRecord; pos >= start + kJournalRecord;) {
+        pos -= kJournalRecord;
+        if (!valid(pos)) {
+            break;
         }
-        r->push(o + hs + opt, (uint32_t)(total - hs - opt - pad), be32(rec + 52), ro);
+        const uint8_t* rec = j + pos;
+        const RecHeader h = rec_header(rec);
+        // PSN checks (:1495-1555)
+        if (h.lease > lease) {
+            return fail_at(BMQCRC_RECOVERY_INVALID_PRIMARY_LEASE_ID, pos);
+        }
+        if (h.lease == lease) {
+            const bool bad = pos >= first_sync ? h.seq != seq - 1 : h.seq > seq - 1;
+            if (bad) {
+                return fail_at(BMQCRC_RECOVERY_INVALID_SEQ_NUMBER, pos);
+            }
+        }
+        lease = h.lease;
+        seq = h.seq;
+
+        if (h.type == kRecJournalOp) {  // :1571-1716
+            const uint64_t sp_seq = ((uint64_t)be32(rec + 28) << 32) | be32(rec + 32);
+            const uint32_t sp_lease = be32(rec + 40);
+            const uint64_t data_off = (uint64_t)be32(rec + 44) * 8;
+            if (rec[23] == 0) {
+                return fail_at(BMQCRC_RECOVERY_INVALID_SYNC_PT_SUB_TYPE, pos);
+            }
+            if (data_off == 0 || dlen < data_off) {
+                return fail_at(BMQCRC_RECOVERY_INVALID_DATA_OFFSET, pos);
+            }
+            if (sp_lease == 0) {
+                return fail_at(BMQCRC_RECOVERY_INVALID_PRIMARY_LEASE_ID, pos);
+            }
+            if (sp_seq == 0) {
+                return fail_at(BMQCRC_RECOVERY_INVALID_SEQ_NUMBER, pos);
+            }
+            if (sp_lease > lease) {
+                return fail_at(BMQCRC_RECOVERY_INVALID_PRIMARY_LEASE_ID, pos);
+            }
+            if (sp_lease == lease && sp_seq != seq) {
+                return fail_at(BMQCRC_RECOVERY_INVALID_SEQ_NUMBER, pos);
+            }
+        } else if (h.type == kRecQueueOp) {  // :1717-2233
+            const uint64_t qkey = key5(rec + 22), akey = key5(rec + 27);
+            if ((int32_t)be32(rec + 32) != kOpPurge || before_queue_deletion(qkey, pos) ||
+                !live(qkey)) {
+                continue;  // only a whole-queue purge of a live queue skips messages
+            }
+            if (akey == 0) {
+                purged_queues.insert(qkey);
+            }
+        } else if (h.type == kRecDeletion) {  // :2234-2305
+            const uint64_t qkey = key5(rec + 23);
+            const Guid g = guid_at(rec + 28);
+            if (g.unset() || qkey == 0) {
+                return fail_at(BMQCRC_RECOVERY_INVALID_DELETION_RECORD, pos);
+            }
+            if (before_queue_deletion(qkey, pos) || purged_queues.count(qkey)) {
+                continue;
+            }
+            deleted_guids.insert(g);  // kept even for an unknown queue (alarmed)
+        } else if (h.type == kRecConfirm) {  // :2306-2389
+            if (guid_at(rec + 32).unset() || key5(rec + 22) == 0) {
+                return fail_at(BMQCRC_RECOVERY_INVALID_CONFIRM_RECORD, pos);
+            }
+        } else if (h.type == kRecMessage) {  // :2390-2645
+            const uint64_t qkey = key5(rec + 22);
+            const Guid g = guid_at(rec + 36);
+            if (g.unset() || qkey == 0) {
+                return fail_at(BMQCRC_RECOVERY_INVALID_MESSAGE_RECORD, pos);
+            }
+            const uint64_t o = (uint64_t)be32(rec + 32) * 8;
+            if (o == 0 || o > dlen) {
+                return fail_at(BMQCRC_RECOVERY_INVALID_DATA_OFFSET, pos);
+            }
+            if (before_queue_deletion(qkey, pos) || purged_queues.count(qkey)) {
+                continue;  // the DATA file is never touched for these (:2390-2393)
+            }
+            auto del = deleted_guids.find(g);
+            if (del != deleted_guids.end()) {
+                deleted_guids.erase(del);
+                continue;
+            }
+            // DATA record checks (:2494-2575).  Where the reference would read
+            // past the end of the DATA file, the record is invalid here.
+            if (o + 8 > dlen) {
+                return fail_at(BMQCRC_RECOVERY_INVALID_DATA_RECORD, pos);
+            }
+            const uint32_t w0 = be32(d + o), w1 = be32(d + o + 4);
+            const uint64_t hs = (uint64_t)(w0 >> 29) * 4;
+            const uint64_t total = (uint64_t)(w0 & 0x1FFFFFFFu) * 4;
+            const uint64_t opt = (uint64_t)(w1 >> 8) * 4;
+            if (hs == 0 || total == 0 || hs + opt >= total || o + total > dlen) {
+                return fail_at(BMQCRC_RECOVERY_INVALID_DATA_RECORD, pos);
+            }
+            const uint32_t pad = d[o + total - 1];
+            if (pad < 1 || pad > 8 || total < hs + opt + pad) {
+                return fail_at(BMQCRC_RECOVERY_INVALID_DATA_RECORD, pos);
+            }
+            if (!live(qkey)) {
+                return fail_at(BMQCRC_RECOVERY_INVALID_QUEUE_KEY, pos);
+            }
+            r->push(o + hs + opt, (uint32_t)(total - hs - opt - pad), be32(rec + 52), pos);
+        }
+    }
+    return 0;
+}
+
+int recovery_view(const bmqcrc_recovery_cfg* cfg, QueueView* qv)
+{
+    if (!cfg) {
+        return 0;
+    }
+    if (cfg->struct_size < sizeof(bmqcrc_recovery_cfg)) {
+        return bmqcrc_set_error(BMQCRC_EINVAL, "cfg->struct_size too small");
+    }
+    qv->with_csl = cfg->with_csl != 0;
+    if (qv->with_csl) {
+        if (cfg->n_queue_keys && !cfg->queue_keys) {
+            return bmqcrc_set_error(BMQCRC_EINVAL, "null queue_keys");
+        }
+        for (uint64_t i = 0; i < cfg->n_queue_keys; ++i) {
+            qv->keys.insert(key5(cfg->queue_keys + 5 * i));
+        }
     }
     return 0;
 }
@@ -312,7 +614,8 @@ int overlap_prepare(void* p, const uint64_t** off, const uint32_t** len, const u
 }
 
 int verify_overlapped(const void* arena, uint64_t bytes, Overlap* ov, uint64_t* n_bad,
-                      std::vector<uint64_t>* bad, uint64_t bad_cap, const bmqcrc_opts* opts)
+                      std::vector<uint64_t>* bad, uint64_t bad_cap, const bmqcrc_opts* opts,
+                      uint64_t* n_written)
 {
     bmqcrc_opts o;
     int rc;
@@ -320,7 +623,7 @@ int verify_overlapped(const void* arena, uint64_t bytes, Overlap* ov, uint64_t* 
         return rc;
     }
     return bmqcrc_verify_host_overlapped(arena, bytes, overlap_prepare, ov, n_bad, bad, bad_cap,
-                                         &o);
+                                         &o, nullptr, n_written);
 }
 
 }  // namespace
@@ -377,52 +680,107 @@ int bmqcrc_put_event_verify(const void* event, uint64_t len, uint64_t* n_msgs, u
     Overlap ov;  // the event's copy to the device overlaps the walk
     ov.walk = [&](Ranges* r) { return walk_put_event((const uint8_t*)event, len, r); };
     std::vector<uint64_t> bad;
-    const int rc = verify_overlapped(event, len, &ov, n_bad, &bad, bad_cap, opts);
+    uint64_t n_written = 0;
+    const int rc = verify_overlapped(event, len, &ov, n_bad, &bad, bad_cap, opts, &n_written);
     *n_msgs = ov.walked ? ov.r.off.size() : 0;
     if (rc) {
         return rc;
     }
-    std::copy(bad.begin(), bad.begin() + std::min<uint64_t>(*n_bad, bad.size()), bad_idx);
+    std::copy(bad.begin(), bad.begin() + n_written, bad_idx);
     return 0;
 }
 
 int64_t bmqcrc_journal_scan(const void* journal, uint64_t jlen, const void* data, uint64_t dlen,
-                            uint64_t* record_off, uint64_t* app_off, uint32_t* app_len,
-                            uint32_t* crc, uint64_t cap)
+                            const bmqcrc_recovery_cfg* cfg, int* recovery_rc,
+                            uint64_t* error_record_off, uint64_t* record_off, uint64_t* app_off,
+                            uint32_t* app_len, uint32_t* crc, uint64_t cap)
 {
     bmqcrc_clear_error();
-    if ((!journal && jlen) || (!data && dlen)) {
-        return bmqcrc_set_error(BMQCRC_EINVAL, "null file buffer");
+    if ((!journal && jlen) || (!data && dlen) || !recovery_rc) {
+        return bmqcrc_set_error(BMQCRC_EINVAL, "null pointer argument");
     }
+    QueueView qv;
     Ranges r;
-    int rc = walk_partition((const uint8_t*)journal, jlen, (const uint8_t*)data, dlen, &r);
-    return rc ? rc : emit(r, cap, app_off, app_len, crc, record_off);
+    RecoveryResult res;
+    int rc = recovery_view(cfg, &qv);
+    if (!rc) {
+        rc = walk_recovery((const uint8_t*)journal, jlen, (const uint8_t*)data, dlen, &qv, &r,
+                           &res);
+    }
+    if (rc) {
+        return rc;
+    }
+    *recovery_rc = res.rc;
+    if (error_record_off) {
+        *error_record_off = res.error_record;
+    }
+    return emit(r, cap, app_off, app_len, crc, record_off);
+}
+
+int bmqcrc_journal_bounds(const void* journal, uint64_t jlen, uint64_t* last_sync_point,
+                          uint64_t* last_record_off)
+{
+    bmqcrc_clear_error();
+    if ((!journal && jlen) || !last_sync_point || !last_record_off) {
+        return bmqcrc_set_error(BMQCRC_EINVAL, "null pointer argument");
+    }
+    const uint8_t* j = (const uint8_t*)journal;
+    uint64_t fh = 0;
+    int rc = file_header_size(j, jlen, kFileJournal, &fh);
+    if (rc) {
+        return rc;
+    }
+    if (fh + 2 > jlen || j[fh] == 0 || fh + (uint64_t)j[fh] * 4 > jlen) {
+        return bad_format("bad JournalFileHeader", fh);
+    }
+    if ((uint64_t)j[fh + 1] * 4 != kJournalRecord) {
+        return bad_format("journal recordWords != 15", fh + 1);
+    }
+    const uint64_t start = fh + (uint64_t)j[fh] * 4;
+    *last_sync_point = last_sync_point_of(j, jlen, start);
+    *last_record_off = last_record(j, jlen, start, *last_sync_point);
+    return 0;
 }
 
 int bmqcrc_recover_verify(const void* journal, uint64_t jlen, const void* data, uint64_t dlen,
-                          uint64_t* n_msgs, uint64_t* n_bad, uint64_t* bad_record_off,
-                          uint64_t bad_cap, const bmqcrc_opts* opts)
+                          const bmqcrc_recovery_cfg* cfg, int* recovery_rc,
+                          uint64_t* error_record_off, uint64_t* n_msgs, uint64_t* n_bad,
+                          uint64_t* bad_record_off, uint64_t bad_cap, const bmqcrc_opts* opts)
 {
     bmqcrc_clear_error();
-    if ((!journal && jlen) || (!data && dlen) || !n_msgs || !n_bad ||
+    if ((!journal && jlen) || (!data && dlen) || !recovery_rc || !n_msgs || !n_bad ||
         (bad_cap && !bad_record_off)) {
         return bmqcrc_set_error(BMQCRC_EINVAL, "null pointer argument");
     }
     *n_msgs = *n_bad = 0;
-    // the DATA file's copy to the device overlaps the journal walk
-    Overlap ov;
-    ov.walk = [&](Ranges* r) {
-        return walk_partition((const uint8_t*)journal, jlen, (const uint8_t*)data, dlen, r);
-    };
-    std::vector<uint64_t> bad;
-    const int rc = verify_overlapped(data, dlen, &ov, n_bad, &bad, bad_cap, opts);
-    const Ranges& r = ov.r;
-    *n_msgs = ov.walked ? r.off.size() : 0;
+    *recovery_rc = 0;
+    QueueView qv;
+    RecoveryResult res;
+    int rc = recovery_view(cfg, &qv);
     if (rc) {
         return rc;
     }
-    const uint64_t k = std::min<uint64_t>(*n_bad, bad.size());
-    for (uint64_t i = 0; i < k; ++i) {
+    // the DATA file's copy to the device overlaps the journal walk
+    Overlap ov;
+    ov.walk = [&](Ranges* r) {
+        return walk_recovery((const uint8_t*)journal, jlen, (const uint8_t*)data, dlen, &qv, r,
+                             &res);
+    };
+    std::vector<uint64_t> bad;
+    uint64_t n_written = 0;
+    rc = verify_overlapped(data, dlen, &ov, n_bad, &bad, bad_cap, opts, &n_written);
+    const Ranges& r = ov.r;
+    *n_msgs = ov.walked ? r.off.size() : 0;
+    if (ov.walked) {
+        *recovery_rc = res.rc;
+        if (error_record_off) {
+            *error_record_off = res.error_record;
+        }
+    }
+    if (rc) {
+        return rc;
+    }
+    for (uint64_t i = 0; i < n_written; ++i) {
         bad_record_off[i] = r.pos[bad[i]];
     }
     return 0;
@@ -458,7 +816,7 @@ int bmqcrc_csl_validate(const void* log, uint64_t len, const uint8_t* expected_l
     };
     uint64_t n_bad = 0;
     std::vector<uint64_t> bad;
-    const int rc = verify_overlapped(log, len, &ov, &n_bad, &bad, 1, opts);
+    const int rc = verify_overlapped(log, len, &ov, &n_bad, &bad, 1, opts, nullptr);
     if (rc) {
         return rc;
     }

@@ -9,6 +9,18 @@
 
 namespace BloombergLP {
 namespace bmqp {
+namespace {
+
+// The GPU itself is unusable (no device, no device memory, a HIP error): the
+// reference's interface has no error channel (bmqp_crc32c.h:240-243), so the
+// batch overloads then finish on the host, bit-exact, with the library's own
+// SSE4.2 CRC.  Argument errors (BMQCRC_EINVAL) are returned as they are.
+bool gpuFailure(int rc)
+{
+    return rc == BMQCRC_ENODEV || rc == BMQCRC_ENOMEM || rc == BMQCRC_EIO;
+}
+
+}  // close unnamed namespace
 
 const unsigned int Crc32c::k_NULL_CRC32C = BMQCRC_NULL_CRC32C;
 
@@ -44,8 +56,22 @@ int Crc32c::calculateBatch(const void* arena,
 {
     static_assert(sizeof(unsigned long long) == sizeof(uint64_t), "u64");
     static_assert(sizeof(unsigned int) == sizeof(uint32_t), "u32");
-    return bmqcrc_crc32c_batch(arena, arenaBytes, reinterpret_cast<const uint64_t*>(offsets),
-                               lengths, seeds, crcs, count, opts);
+    const int rc = bmqcrc_crc32c_batch(arena, arenaBytes,
+                                       reinterpret_cast<const uint64_t*>(offsets), lengths, seeds,
+                                       crcs, count, opts);
+    if (!gpuFailure(rc) || (opts && (opts->flags & BMQCRC_F_DEVICE_PTRS))) {
+        return rc;  // device-resident inputs cannot be read on the host
+    }
+    for (unsigned long long i = 0; i < count; ++i) {
+        if (offsets[i] > arenaBytes || lengths[i] > arenaBytes - offsets[i]) {
+            return BMQCRC_EINVAL;
+        }
+    }
+    const char* base = static_cast<const char*>(arena);
+    for (unsigned long long i = 0; i < count; ++i) {
+        crcs[i] = calculate(base + offsets[i], lengths[i], seeds ? seeds[i] : k_NULL_CRC32C);
+    }
+    return 0;
 }
 
 int Crc32c::calculateBatch(const bdlbb::Blob* blobs,
@@ -79,8 +105,15 @@ int Crc32c::calculateBatch(const bdlbb::Blob* blobs,
             }
         }
     }
-    return bmqcrc_crc32c_blobs(arena.data(), total, off.data(), len.data(), len.size(),
-                               first.data(), seeds, crcs, count, opts);
+    const int rc = bmqcrc_crc32c_blobs(arena.data(), total, off.data(), len.data(), len.size(),
+                                       first.data(), seeds, crcs, count, opts);
+    if (!gpuFailure(rc)) {
+        return rc;
+    }
+    for (unsigned int b = 0; b < count; ++b) {
+        crcs[b] = calculate(blobs[b], seeds ? seeds[b] : k_NULL_CRC32C);
+    }
+    return 0;
 }
 
 }  // namespace bmqp

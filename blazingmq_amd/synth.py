@@ -32,10 +32,12 @@ def host_crcs(buf, offsets, lengths):
 
 
 def partition(n, app_len, seed=11, lease_id=1, timestamp=0x6720EAB4,
-              queue_key=b"\x26\xda\xcd\xc9\x74"):
-    """(journal, data, app_offsets, app_lengths) for n MESSAGE records whose
-    application data are `app_len` random bytes each (mqbs_filestoreprotocol.h
-    DataHeader :703, MessageRecord :1125)."""
+              queue_key=S.DEFAULT_QUEUE_KEY):
+    """(journal, data, app_offsets, app_lengths) for one queue: a QueueOp
+    CREATION record, then n MESSAGE records whose application data are
+    `app_len` random bytes each, all outstanding (mqbs_filestoreprotocol.h
+    QueueOpRecord :1694, DataHeader :703, MessageRecord :1125) -- the bytes
+    ``storage.write_partition`` produces."""
     rng = np.random.default_rng(seed)
     rem = (12 + app_len) % S.DWORD
     pad = S.DWORD - rem if rem else S.DWORD
@@ -52,18 +54,22 @@ def partition(n, app_len, seed=11, lease_id=1, timestamp=0x6720EAB4,
     app_lens = np.full(n, app_len, np.uint32)
     crcs = host_crcs(data, app_off, app_lens)
 
-    seq = 1 + np.arange(n, dtype=np.uint64)
-    j = np.zeros((n, S.JOURNAL_RECORD_SIZE), np.uint8)
+    seq = 1 + np.arange(n + 1, dtype=np.uint64)  # record 0: the queue's CREATION
+    j = np.zeros((n + 1, S.JOURNAL_RECORD_SIZE), np.uint8)
     j[:, 0:2] = _be((S.REC_MESSAGE << 12) | 1, ">u2")
+    j[0, 0:2] = _be(S.REC_QUEUE_OP << 12, ">u2")
     j[:, 2:4] = _be(seq >> 32, ">u2")
     j[:, 4:8] = _be(seq & 0xFFFFFFFF, ">u4")
     j[:, 8:12] = _be(lease_id, ">u4")
     j[:, 12:20] = _be(timestamp, ">u8")
     j[:, 22:27] = np.frombuffer(queue_key, np.uint8)
-    j[:, 32:36] = _be(pos // S.DWORD, ">u4")
-    j[:, 36] = 0x40
-    j[:, 44:52] = _be(seq + 1, ">u8")
-    j[:, 52:56] = _be(crcs, ">u4")
+    j[0, 32:36] = _be(S.OP_CREATION, ">u4")
+    j[0, 36:40] = _be(9, ">u4")
+    m = j[1:]
+    m[:, 32:36] = _be(pos // S.DWORD, ">u4")
+    m[:, 36] = 0x40
+    m[:, 44:52] = _be(np.arange(1, n + 1, dtype=np.uint64), ">u8")
+    m[:, 52:56] = _be(crcs, ">u4")
     j[:, 56:60] = _be(S.RECORD_MAGIC, ">u4")
     jhead = np.concatenate([S.file_header(S.FILE_TYPE_JOURNAL),
                             np.array([3, 15] + [0] * 10, np.uint8)])

@@ -20,7 +20,8 @@
  * buffer).  Scans return the number of messages found (which may exceed
  * `cap`; only `cap` entries are written, so cap = 0 sizes the arrays) or a
  * negative BMQCRC_E* code with bmqcrc_last_error() naming the offending
- * offset.  GPU entry points return BMQCRC_ENODEV without a gfx950 device.
+ * offset.  GPU entry points return BMQCRC_ENODEV without a gfx950 device;
+ * the C++ spellings at the end of this header fall back to the host CRC.
  */
 #ifndef BMQCRC_PROTOCOL_H
 #define BMQCRC_PROTOCOL_H
@@ -52,25 +53,74 @@ int64_t bmqcrc_put_event_fill_crcs(void* event, uint64_t len, const bmqcrc_opts*
 int bmqcrc_put_event_verify(const void* event, uint64_t len, uint64_t* n_msgs, uint64_t* n_bad,
                             uint64_t* bad_idx, uint64_t bad_cap, const bmqcrc_opts* opts);
 
-/* ---- partition recovery (mqbs_filestoreprotocol.h:306,426,483,703,1125) -- */
+/* ---- partition recovery (mqbs_filestoreprotocol.h:306,426,483,703,953-1990) */
 
-/* Walk a journal (FileHeader + JournalFileHeader + 60-byte records, stopping
- * at the first all-zero record) and the DATA file it points into.  For each
- * MESSAGE record i: record_off = journal offset of the record, app_off /
- * app_len = application data of its DATA record (DataHeader + options +
- * app data + 1..8 padding bytes, validated like mqbs_filestore.cpp:2495-2575),
- * crc = the CRC32C stored in the record.  Any array may be NULL. */
+/* mqbs::FileStore::recoverMessages result codes (mqbs_filestore.cpp:1073-1091)
+ * that the record selection below can produce. */
+#define BMQCRC_RECOVERY_SUCCESS 0
+#define BMQCRC_RECOVERY_INVALID_PRIMARY_LEASE_ID (-2)
+#define BMQCRC_RECOVERY_INVALID_SEQ_NUMBER (-3)
+#define BMQCRC_RECOVERY_INVALID_QUEUE_OP_RECORD (-4)
+#define BMQCRC_RECOVERY_NULL_QUEUE_KEY (-5)
+#define BMQCRC_RECOVERY_DUPLICATE_QUEUE_KEY (-7)
+#define BMQCRC_RECOVERY_INVALID_QUEUE_KEY (-8)
+#define BMQCRC_RECOVERY_INVALID_DATA_OFFSET (-11)
+#define BMQCRC_RECOVERY_INVALID_SYNC_PT_SUB_TYPE (-12)
+#define BMQCRC_RECOVERY_INVALID_DELETION_RECORD (-14)
+#define BMQCRC_RECOVERY_INVALID_CONFIRM_RECORD (-15)
+#define BMQCRC_RECOVERY_INVALID_MESSAGE_RECORD (-16)
+#define BMQCRC_RECOVERY_INVALID_DATA_RECORD (-17)
+
+/* The queues recoverMessages knows (its `withCSL` argument and
+ * `queueKeyInfoMap`).  cfg == NULL or with_csl == 0: the live queues are the
+ * keys of the journal's own QueueOp CREATION records (the reference's first
+ * pass).  with_csl != 0: the cluster state's live queues, n_queue_keys
+ * 5-byte mqbu::StorageKey values at queue_keys. */
+typedef struct bmqcrc_recovery_cfg {
+    uint32_t struct_size; /* sizeof(bmqcrc_recovery_cfg) */
+    int32_t with_csl;
+    const uint8_t* queue_keys;
+    uint64_t n_queue_keys;
+} bmqcrc_recovery_cfg;
+
+/* The MESSAGE records whose payload FileStore::recoverMessages CRCs
+ * (mqbs_filestore.cpp:2603-2624), selected exactly as it does: the journal
+ * is bounded by its last sync point and last valid record
+ * (mqbs_filestoreprotocolutil.cpp:165-289) and walked backwards twice; a
+ * MESSAGE record is skipped when its GUID has a later DELETION record, its
+ * queue a later whole-queue PURGE, or it precedes its queue's last
+ * QueueOp DELETION -- and for skipped records the DATA file is not read.
+ * Records come out in that backward order: record_off = journal offset,
+ * app_off / app_len = application data of its DATA record (DataHeader +
+ * options + app data + 1..8 padding bytes), crc = the stored CRC32C.
+ * *recovery_rc = the reference's result (0 or BMQCRC_RECOVERY_*) and
+ * *error_record_off the offending record's offset when it is not 0; the
+ * records before that point are still returned (the reference had CRC'd
+ * them).  Any output array may be NULL.  CPU only. */
 int64_t bmqcrc_journal_scan(const void* journal, uint64_t jlen, const void* data, uint64_t dlen,
-                            uint64_t* record_off, uint64_t* app_off, uint32_t* app_len,
-                            uint32_t* crc, uint64_t cap);
+                            const bmqcrc_recovery_cfg* cfg, int* recovery_rc,
+                            uint64_t* error_record_off, uint64_t* record_off, uint64_t* app_off,
+                            uint32_t* app_len, uint32_t* crc, uint64_t cap);
 
-/* Recovery CRC check of a whole partition: one scan, one batched verify.
- * Mismatches are what the reference raises as a RECOVERY alarm and skips
- * (mqbs_filestore.cpp:2613-2624); their journal record offsets are returned
- * in ascending order (up to bad_cap). */
+/* The journal's bounds as JournalFileIterator computes them: *last_sync_point
+ * = offset of the last well-formed SYNCPOINT record, *last_record_off = the
+ * last valid record after it (0 = none; mqbs_filestoreprotocolutil.cpp:165-289).
+ * Records past *last_record_off (a torn write, a pre-allocated zero tail)
+ * are not part of the journal.  CPU only. */
+int bmqcrc_journal_bounds(const void* journal, uint64_t jlen, uint64_t* last_sync_point,
+                          uint64_t* last_record_off);
+
+/* Recovery CRC check of a whole partition: the selection of
+ * bmqcrc_journal_scan, then one batched verify on the GPU.  *n_msgs = records
+ * CRC'd; mismatches are what the reference raises as a RECOVERY alarm and
+ * keeps going (mqbs_filestore.cpp:2613-2624): *n_bad of them, the first
+ * min(*n_bad, bad_cap) in the order the reference raises them (backward
+ * journal order) in bad_record_off.  *recovery_rc / *error_record_off as
+ * in bmqcrc_journal_scan. */
 int bmqcrc_recover_verify(const void* journal, uint64_t jlen, const void* data, uint64_t dlen,
-                          uint64_t* n_msgs, uint64_t* n_bad, uint64_t* bad_record_off,
-                          uint64_t bad_cap, const bmqcrc_opts* opts);
+                          const bmqcrc_recovery_cfg* cfg, int* recovery_rc,
+                          uint64_t* error_record_off, uint64_t* n_msgs, uint64_t* n_bad,
+                          uint64_t* bad_record_off, uint64_t bad_cap, const bmqcrc_opts* opts);
 
 /* ---- cluster state ledger (mqbc_clusterstateledgerprotocol.h:76,272) ------ */
 
@@ -108,8 +158,27 @@ int bmqcrc_csl_validate(const void* log, uint64_t len, const uint8_t* expected_l
 #ifdef __cplusplus
 }  /* extern "C" */
 
+#include <vector>
+
 /* ---- C++ spellings at the reference call sites -------------------------- */
+/* The reference's calls have no error channel (bmqp_crc32c.h:240-243), so
+ * these spellings never surface a GPU failure: when the batched MI355X call
+ * fails for want of a GPU (BMQCRC_ENODEV, ENOMEM, EIO) they redo the same
+ * walk and CRC every message on the host with the library's own SSE4.2 code
+ * (bmqcrc_crc32c), bit-exact.  Format errors (BMQCRC_EINVAL) are returned.
+ * The C-ABI batch entry points above stay GPU-only. */
 namespace BloombergLP {
+namespace bmqcrc_detail {
+inline bool gpuFailure(int64_t rc)
+{
+    return rc == BMQCRC_ENODEV || rc == BMQCRC_ENOMEM || rc == BMQCRC_EIO;
+}
+inline uint32_t be32(const uint8_t* p)
+{
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+}  // close namespace bmqcrc_detail
+
 namespace bmqp {
 /// Batched counterpart of the CRC step of `PutEventBuilder::packMessage`
 /// (bmqp_puteventbuilder.cpp:302-320) and `PutMessageIterator` (:678), over a
@@ -117,28 +186,98 @@ namespace bmqp {
 struct PutEventCrc32c {
     static int64_t fillAll(void* event, uint64_t len, const bmqcrc_opts* opts = 0)
     {
-        return bmqcrc_put_event_fill_crcs(event, len, opts);
+        const int64_t rc = bmqcrc_put_event_fill_crcs(event, len, opts);
+        if (!bmqcrc_detail::gpuFailure(rc)) {
+            return rc;
+        }
+        const int64_t n = bmqcrc_put_event_scan(event, len, 0, 0, 0, 0);
+        if (n <= 0) {
+            return n;
+        }
+        std::vector<uint64_t> off(n), pos(n);
+        std::vector<uint32_t> ln(n);
+        bmqcrc_put_event_scan(event, len, off.data(), ln.data(), pos.data(), n);
+        uint8_t* ev = static_cast<uint8_t*>(event);
+        for (int64_t i = 0; i < n; ++i) {
+            const uint32_t c = bmqcrc_crc32c(ev + off[i], ln[i], 0);
+            ev[pos[i]] = (uint8_t)(c >> 24);
+            ev[pos[i] + 1] = (uint8_t)(c >> 16);
+            ev[pos[i] + 2] = (uint8_t)(c >> 8);
+            ev[pos[i] + 3] = (uint8_t)c;
+        }
+        return n;
     }
     static int verifyAll(const void* event, uint64_t len, uint64_t* numMessages,
                          uint64_t* numBad, uint64_t* badIndices = 0, uint64_t badCap = 0,
                          const bmqcrc_opts* opts = 0)
     {
-        return bmqcrc_put_event_verify(event, len, numMessages, numBad, badIndices, badCap,
-                                       opts);
+        const int rc = bmqcrc_put_event_verify(event, len, numMessages, numBad, badIndices,
+                                               badCap, opts);
+        if (!bmqcrc_detail::gpuFailure(rc)) {
+            return rc;
+        }
+        const int64_t n = bmqcrc_put_event_scan(event, len, 0, 0, 0, 0);
+        if (n < 0) {
+            return (int)n;
+        }
+        std::vector<uint64_t> off(n), pos(n);
+        std::vector<uint32_t> ln(n);
+        bmqcrc_put_event_scan(event, len, off.data(), ln.data(), pos.data(), n);
+        const uint8_t* ev = static_cast<const uint8_t*>(event);
+        uint64_t bad = 0;
+        for (int64_t i = 0; i < n; ++i) {
+            if (bmqcrc_crc32c(ev + off[i], ln[i], 0) != bmqcrc_detail::be32(ev + pos[i])) {
+                if (bad < badCap) {
+                    badIndices[bad] = (uint64_t)i;
+                }
+                ++bad;
+            }
+        }
+        *numMessages = (uint64_t)n;
+        *numBad = bad;
+        return 0;
     }
 };
 }  // close namespace bmqp
 
 namespace mqbs {
-/// Batched CRC check of `FileStore::recoverMessages` (mqbs_filestore.cpp:2603).
+/// Batched CRC check of `FileStore::recoverMessages` (mqbs_filestore.cpp:2603),
+/// over the same records the reference CRCs (see bmqcrc_recover_verify).
 struct FileStoreCrc32c {
     static int verifyRecovery(const void* journal, uint64_t journalLen, const void* data,
-                              uint64_t dataLen, uint64_t* numMessages, uint64_t* numBad,
-                              uint64_t* badRecordOffsets = 0, uint64_t badCap = 0,
-                              const bmqcrc_opts* opts = 0)
+                              uint64_t dataLen, int* recoveryRc, uint64_t* numMessages,
+                              uint64_t* numBad, uint64_t* badRecordOffsets = 0,
+                              uint64_t badCap = 0, const bmqcrc_recovery_cfg* cfg = 0,
+                              const bmqcrc_opts* opts = 0, uint64_t* errorRecordOffset = 0)
     {
-        return bmqcrc_recover_verify(journal, journalLen, data, dataLen, numMessages, numBad,
-                                     badRecordOffsets, badCap, opts);
+        const int rc = bmqcrc_recover_verify(journal, journalLen, data, dataLen, cfg, recoveryRc,
+                                             errorRecordOffset, numMessages, numBad,
+                                             badRecordOffsets, badCap, opts);
+        if (!bmqcrc_detail::gpuFailure(rc)) {
+            return rc;
+        }
+        const int64_t n = bmqcrc_journal_scan(journal, journalLen, data, dataLen, cfg,
+                                              recoveryRc, errorRecordOffset, 0, 0, 0, 0, 0);
+        if (n < 0) {
+            return (int)n;
+        }
+        std::vector<uint64_t> rec(n), off(n);
+        std::vector<uint32_t> ln(n), crc(n);
+        bmqcrc_journal_scan(journal, journalLen, data, dataLen, cfg, recoveryRc,
+                            errorRecordOffset, rec.data(), off.data(), ln.data(), crc.data(), n);
+        const uint8_t* d = static_cast<const uint8_t*>(data);
+        uint64_t bad = 0;
+        for (int64_t i = 0; i < n; ++i) {
+            if (bmqcrc_crc32c(d + off[i], ln[i], 0) != crc[i]) {
+                if (bad < badCap) {
+                    badRecordOffsets[bad] = rec[i];
+                }
+                ++bad;
+            }
+        }
+        *numMessages = (uint64_t)n;
+        *numBad = bad;
+        return 0;
     }
 };
 }  // close namespace mqbs
@@ -152,7 +291,29 @@ struct ClusterStateLedgerCrc32c {
     {
         int cslRc = 0;
         const int rc = bmqcrc_csl_validate(log, len, expectedLogId, &cslRc, offset, 0, opts);
-        return rc ? rc * 1000 : cslRc;
+        if (!bmqcrc_detail::gpuFailure(rc)) {
+            return rc ? rc * 1000 : cslRc;
+        }
+        int walkRc = 0;
+        uint64_t end = 0;
+        const int64_t n = bmqcrc_csl_scan(log, len, expectedLogId, 0, 0, 0, 0, &walkRc, &end);
+        if (n < 0) {
+            return (int)n * 1000;
+        }
+        std::vector<uint64_t> off(n);
+        std::vector<uint32_t> ln(n), crc(n);
+        bmqcrc_csl_scan(log, len, expectedLogId, off.data(), ln.data(), crc.data(), n, &walkRc,
+                        &end);
+        const uint8_t* a = static_cast<const uint8_t*>(log);
+        for (int64_t i = 0; i < n; ++i) {  // the first corrupt record in log order
+            if (bmqcrc_crc32c(a + off[i], ln[i], 0) != crc[i]) {
+                return BMQCRC_CSL_INVALID_CHECKSUM;
+            }
+        }
+        if (walkRc == 0) {
+            *offset = end;
+        }
+        return walkRc;
     }
 };
 }  // close namespace mqbc

@@ -38,7 +38,10 @@ struct Crc32c {
     /// Batched: `crcs[i] = calculate(arena + offsets[i], lengths[i],
     /// seeds ? seeds[i] : 0)` for `i < count`, computed on an MI355X in one
     /// launch (`opts` selects device/stream/pointer kind, may be 0).  Returns
-    /// 0 on success or a negative BMQCRC_E* code; never falls back to the CPU.
+    /// 0 on success or a negative BMQCRC_E* code.  Like the reference's
+    /// calls it has no GPU failure mode: with host buffers and no usable GPU
+    /// (BMQCRC_ENODEV/ENOMEM/EIO from the batch) it finishes on the host
+    /// with the scalar path, bit-exact; device-resident inputs return the code.
     static int calculateBatch(const void* arena,
                               unsigned long long arenaBytes,
                               const unsigned long long* offsets,
@@ -51,7 +54,8 @@ struct Crc32c {
     /// Batched Blob overload: `crcs[i] = calculate(blobs[i], seeds ? seeds[i] :
     /// 0)` for `i < count`, computed on an MI355X (the blobs' buffers are
     /// gathered into one staging arena, CRC'd per buffer and chained on the
-    /// device).  Returns 0 or a negative BMQCRC_E* code; no CPU fallback.
+    /// device).  Returns 0 or a negative BMQCRC_E* code; without a usable GPU
+    /// it finishes on the host like the overload above.
     static int calculateBatch(const bdlbb::Blob* blobs,
                               unsigned int       count,
                               const unsigned int* seeds,

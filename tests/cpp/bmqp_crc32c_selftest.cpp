@@ -4,7 +4,7 @@
 // reference's own golden constants.
 //
 //   bmqp_selftest            CPU cases 1-5, 7, 8 (+ fuzz property)
-//   bmqp_selftest gpu        additionally calculateBatch on the MI355X
+//   bmqp_selftest gpu        requires the MI355X for the batch paths
 #include "bmqcrc_protocol.h"
 #include "bmqp_crc32c.h"
 
@@ -307,7 +307,9 @@ static void protocol_scans(std::vector<std::string>* apps, std::string* ev, std:
     CHECK_EQ(end, log->size());
 }
 
-static void gpu_protocol(const std::vector<std::string>& apps, std::string ev, std::string log)
+// The C++ call-site spellings: on the GPU, or on the host when there is none.
+static void protocol_spellings(const std::vector<std::string>& apps, std::string ev,
+                               std::string log)
 {
     using namespace BloombergLP;
     CHECK_EQ(bmqp::PutEventCrc32c::fillAll(&ev[0], ev.size()), apps.size());
@@ -368,44 +370,50 @@ static bool fixture(std::string* journal, std::string* data)
 
 static void recovery_scan(const std::string& j, const std::string& d)
 {
-    uint64_t rec[4], off[4];
+    // FileStore::recoverMessages CRCs only the second message: the first
+    // one's GUID has a DELETION record at offset 404 (mqbs_filestore.cpp:2481).
+    uint64_t rec[4], off[4], err = 7;
     uint32_t len[4], crc[4];
-    CHECK_EQ(bmqcrc_journal_scan(j.data(), j.size(), d.data(), d.size(), rec, off, len, crc, 4),
-             2);
-    CHECK_EQ(rec[0], 224u);
-    CHECK_EQ(rec[1], 644u);
-    for (int i = 0; i < 2; ++i) {
-        CHECK_EQ(len[i], 11u);
-        CHECK_EQ(crc[i], 3381945770u);
-        CHECK_EQ(memcmp(d.data() + off[i], "hello world", 11), 0);
-        CHECK_EQ(Crc32c::calculate(d.data() + off[i], len[i]), 3381945770u);
-    }
+    int rrc = 1;
+    CHECK_EQ(bmqcrc_journal_scan(j.data(), j.size(), d.data(), d.size(), 0, &rrc, &err, rec, off,
+                                 len, crc, 4),
+             1);
+    CHECK_EQ(rrc, 0);
+    CHECK_EQ(rec[0], 644u);
+    CHECK_EQ(len[0], 11u);
+    CHECK_EQ(crc[0], 3381945770u);
+    CHECK_EQ(memcmp(d.data() + off[0], "hello world", 11), 0);
+    CHECK_EQ(Crc32c::calculate(d.data() + off[0], len[0]), 3381945770u);
 }
 
-static void gpu_recovery(const std::string& j, std::string d)
+// The C++ spelling: on the GPU, or on the host when there is none.
+static void recovery_verify(const std::string& j, std::string d)
 {
     using namespace BloombergLP;
     uint64_t n = 0, bad = 0, where[2] = {0, 0};
-    CHECK_EQ(mqbs::FileStoreCrc32c::verifyRecovery(j.data(), j.size(), d.data(), d.size(), &n,
-                                                   &bad, where, 2),
+    int rrc = 1;
+    CHECK_EQ(mqbs::FileStoreCrc32c::verifyRecovery(j.data(), j.size(), d.data(), d.size(), &rrc,
+                                                   &n, &bad, where, 2),
              0);
-    CHECK_EQ(n, 2u);
+    CHECK_EQ(rrc, 0);
+    CHECK_EQ(n, 1u);
     CHECK_EQ(bad, 0u);
-    d[76 + 4] ^= 0x20;  // second record's app data: "hello World"
-    CHECK_EQ(mqbs::FileStoreCrc32c::verifyRecovery(j.data(), j.size(), d.data(), d.size(), &n,
-                                                   &bad, where, 2),
+    d[52 + 4] ^= 0x20;  // the deleted message's payload: never CRC'd, no alarm
+    CHECK_EQ(mqbs::FileStoreCrc32c::verifyRecovery(j.data(), j.size(), d.data(), d.size(), &rrc,
+                                                   &n, &bad, where, 2),
+             0);
+    CHECK_EQ(bad, 0u);
+    d[76 + 4] ^= 0x20;  // the live message's payload: "hello World"
+    CHECK_EQ(mqbs::FileStoreCrc32c::verifyRecovery(j.data(), j.size(), d.data(), d.size(), &rrc,
+                                                   &n, &bad, where, 2),
              0);
     CHECK_EQ(bad, 1u);
     CHECK_EQ(where[0], 644u);
 }
 
-static void gpu_batch()
+// calculateBatch overloads: on the GPU, or on the host when there is none.
+static void batch_overloads()
 {
-    if (bmqcrc_device_count() <= 0) {
-        fprintf(stderr, "gpu: no device\n");
-        ++g_fail;
-        return;
-    }
     std::string arena;
     std::vector<unsigned long long> off;
     std::vector<unsigned> len, exp;
@@ -470,21 +478,28 @@ int main(int argc, char** argv)
     if (have_fixture) {
         recovery_scan(journal, data);
     }
-    if (argc > 1 && strcmp(argv[1], "gpu") == 0) {
-        gpu_batch();
-        gpu_protocol(apps, ev, log);
-        if (have_fixture) {
-            gpu_recovery(journal, data);
-        }
-    } else {
-        // without a GPU the batch path must refuse loudly, never fall back
-        unsigned out = 0;
-        unsigned long long o = 0;
-        unsigned l = 1;
-        const int rc = Crc32c::calculateBatch("x", 1, &o, &l, 0, &out, 1);
-        if (bmqcrc_device_count() == 0) {
-            CHECK_EQ((unsigned)rc, (unsigned)BMQCRC_ENODEV);
-        }
+    const bool gpu = argc > 1 && strcmp(argv[1], "gpu") == 0;
+    if (gpu && bmqcrc_device_count() <= 0) {
+        fprintf(stderr, "gpu: no device\n");
+        ++g_fail;
+    }
+    if (!gpu && bmqcrc_device_count() == 0) {
+        // without a GPU the C-ABI batch path refuses loudly, never falls back
+        uint32_t out = 0;
+        uint64_t o = 0;
+        uint32_t l = 1;
+        CHECK_EQ((unsigned)bmqcrc_crc32c_batch("x", 1, &o, &l, 0, &out, 1, 0),
+                 (unsigned)BMQCRC_ENODEV);
+        std::string ev2 = ev;
+        CHECK_EQ((unsigned)bmqcrc_put_event_fill_crcs(&ev2[0], ev2.size(), 0),
+                 (unsigned)BMQCRC_ENODEV);
+    }
+    // ... while the C++ spellings at the reference call sites give the same
+    // bit-exact answers on either path
+    batch_overloads();
+    protocol_spellings(apps, ev, log);
+    if (have_fixture) {
+        recovery_verify(journal, data);
     }
     printf("%s: %d failure(s)\n", g_fail ? "FAIL" : "PASS", g_fail);
     return g_fail ? 1 : 0;

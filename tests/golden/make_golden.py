@@ -105,6 +105,31 @@ def main():
     assert msg_offsets == [224, 644], msg_offsets
     out["journal_file"] = {"file": "test.bmq_journal", "message_record_offsets": msg_offsets,
                            "crc": crcs}
+    # Which MESSAGE records recovery keeps (FileStore::recoverMessages CRCs
+    # exactly these): bmqstoragetool's summary counts 1 outstanding message
+    # (summary_result.txt) and names it (test_journalfile.py
+    # test_confirmed_outstanding_result: TEST_GUID_1 outstanding, TEST_GUID_2
+    # confirmed and deleted); the summary also prints the journal bounds.
+    summary = open(os.path.join(DATA_DIR, "summary_result.txt")).read()
+    tests_py = open(os.path.join(DATA_DIR, "..", "test_journalfile.py")).read()
+    guids = dict(re.findall(r'(TEST_GUID_\d)\s*=\s*b"([0-9A-F]{32})"', tests_py))
+    outstanding = int(re.search(r"Number of outstanding messages:\s*(\d+)", summary).group(1))
+    guid_at = {}
+    for b in blocks:
+        if b.startswith("MESSAGE"):
+            guid_at[re.search(r"GUID\s*:\s*([0-9A-F]{32})", b).group(1)] = \
+                int(re.search(r"Offset\s*:\s*(\d+)", b).group(1))
+    out["recovery"] = {
+        "outstanding_messages": outstanding,
+        "outstanding_guids": [guids["TEST_GUID_1"]],
+        "deleted_guids": [guids["TEST_GUID_2"]],
+        "outstanding_record_offsets": [guid_at[guids["TEST_GUID_1"]]],
+        "last_valid_record_offset": int(re.search(r"Last Valid Record Offset\s*:\s*(\d+)",
+                                                  summary).group(1)),
+        "last_valid_syncpoint_offset": int(re.search(r"Last Valid SyncPoint Offset\s*:\s*(\d+)",
+                                                     summary).group(1)),
+    }
+    assert outstanding == 1 and out["recovery"]["outstanding_record_offsets"] == [644], out["recovery"]
     out["data_file"] = {
         "file": "test.bmq_data",
         "records": [{"record_offset": 40, "header_bytes": 12, "app_data_len": 11, "crc": crcs[0]},

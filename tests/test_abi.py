@@ -28,7 +28,7 @@ def test_header_declares_expected_api():
               "bmqcrc_kernel_timing", "bmqcrc_device_count", "bmqcrc_last_error",
               "bmqcrc_version", "bmqcrc_crc32c_verify", "bmqcrc_crc32c_blobs",
               "bmqcrc_put_event_scan", "bmqcrc_put_event_fill_crcs", "bmqcrc_put_event_verify",
-              "bmqcrc_journal_scan", "bmqcrc_recover_verify", "bmqcrc_csl_scan",
+              "bmqcrc_journal_scan", "bmqcrc_journal_bounds", "bmqcrc_recover_verify", "bmqcrc_csl_scan",
               "bmqcrc_csl_validate", "bmqcrc_host_register", "bmqcrc_host_unregister"):
         assert n in names
 
@@ -53,6 +53,6 @@ def test_library_contains_gfx950_code_object():
 def test_version_and_error_string():
     lib = ctypes.CDLL(LIB)
     lib.bmqcrc_version.restype = ctypes.c_uint32
-    assert lib.bmqcrc_version() >> 16 == 1
+    assert lib.bmqcrc_version() >> 16 == 2
     lib.bmqcrc_last_error.restype = ctypes.c_char_p
     assert isinstance(lib.bmqcrc_last_error(), bytes)

@@ -86,6 +86,22 @@ def test_cpp_dropin_selftest():
     assert "PASS" in r.stdout
 
 
+def test_cpp_spellings_fall_back_without_gpu():
+    """the reference's calls have no error channel, so the C++
+    spellings at its call sites (bmqp::Crc32c::calculateBatch,
+    PutEventCrc32c, FileStoreCrc32c, ClusterStateLedgerCrc32c) finish on the
+    host, bit-exact, when no GPU is visible -- while the C-ABI batch calls
+    still return BMQCRC_ENODEV (both checked inside the self-test)."""
+    exe = os.path.join(ROOT, "tests", "cpp", "bin", "bmqp_selftest")
+    if not os.path.exists(exe):
+        pytest.skip("selftest not built")
+    env = dict(os.environ, BMQCRC_GOLDEN_DIR=os.path.join(ROOT, "tests", "golden"),
+               HIP_VISIBLE_DEVICES="", ROCR_VISIBLE_DEVICES="")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "PASS" in r.stdout
+
+
 @pytest.mark.skipif(device_count() > 0, reason="GPU present: batch path is exercised by -m gpu")
 def test_batch_refuses_without_gpu():
     # the batch path never falls back to the CPU
@@ -125,3 +141,37 @@ def test_host_register_refuses_without_gpu():
         assert N.lib.bmqcrc_host_register(a.ctypes.data, a.size, -1,
                                           ctypes.byref(p)) == N.BMQCRC_ENODEV
         assert N.lib.bmqcrc_host_unregister(a.ctypes.data) == N.BMQCRC_ENODEV
+
+
+@pytest.mark.parametrize("bad", ["short", "dtype", "strided", "readonly", "list"])
+def test_host_batch_rejects_bad_out(bad):
+    """A caller-supplied `out` the C library would overrun is refused before
+    the call (it writes 4 * n bytes)."""
+    a = np.zeros(256, np.uint8)
+    off, ln = np.arange(4, dtype=np.uint64) * 8, np.full(4, 8, np.uint32)
+    out = {"short": np.zeros(3, np.uint32), "dtype": np.zeros(4, np.int64),
+           "strided": np.zeros(8, np.uint32)[::2], "list": [0, 0, 0, 0]}.get(bad)
+    if bad == "readonly":
+        out = np.zeros(4, np.uint32)
+        out.flags.writeable = False
+    with pytest.raises(TypeError):
+        Crc32c.calculate_batch(a, off, ln, out=out)
+
+
+def test_torch_batch_rejects_bad_out_and_seeds():
+    """Same for the torch form (CPU tensors stand in for device tensors: the
+    checks run before any device call)."""
+    import torch
+    from blazingmq_amd import crc32c as C
+    dev = torch.device("cpu")
+    a = torch.zeros(256, dtype=torch.uint8)
+    off = torch.arange(4, dtype=torch.int64) * 8
+    ln = torch.full((4,), 8, dtype=torch.int32)
+    for out in (torch.zeros(3, dtype=torch.int32), torch.zeros(4, dtype=torch.int64),
+                torch.zeros(8, dtype=torch.int32)[::2]):
+        with pytest.raises(TypeError):
+            C._batch_torch(torch, a, off, ln, None, out, 0, None, True)
+    with pytest.raises(TypeError):
+        C._batch_torch(torch, a, off, ln, torch.zeros(8, dtype=torch.int32)[::2], None, 0, None,
+                       True)
+    assert dev.type == "cpu"

@@ -16,11 +16,47 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 
-def test_verify_fixture_partition(cuda):
+def test_verify_fixture_partition(cuda, golden):
     j = np.fromfile(os.path.join(GOLD, "test.bmq_journal"), np.uint8)
     d = np.fromfile(os.path.join(GOLD, "test.bmq_data"), np.uint8)
     res = storage.verify_partition(j, d)
-    assert res["n_messages"] == 2 and res["n_bad"] == 0
+    # the first message is deleted: only the outstanding one is CRC'd
+    assert res["n_messages"] == golden["recovery"]["outstanding_messages"] == 1
+    assert res["n_bad"] == 0 and res["recovery_rc"] == 0
+    d2 = d.copy()
+    d2[52 + 3] ^= 1   # the deleted message's payload: no alarm
+    assert storage.verify_partition(j, d2)["n_bad"] == 0
+    d2[76 + 3] ^= 1   # the outstanding one's: alarm at its record
+    res = storage.verify_partition(j, d2)
+    assert res["n_bad"] == 1 and res["bad_record_offsets"].tolist() == [644]
+
+
+def test_verify_rich_partition_alarms_only_on_live_messages(cuda):
+    """Every skip rule of recoverMessages at once (deleted GUIDs, whole-queue
+    purges, records before their queue's DELETION, a new lease), with the
+    payload of every skipped message corrupted and one skipped DataHeader
+    malformed: the GPU verify raises no alarm for them, CRCs exactly the
+    outstanding messages bit-exact, and finds planted corruptions in live
+    messages at their exact record offsets."""
+    from test_recovery_selection import rich_partition
+    j, d, expected, apps = rich_partition(seed=1)
+    res = storage.verify_partition(j, d)
+    assert res["recovery_rc"] == 0
+    assert res["n_messages"] == len(expected) and res["n_bad"] == 0
+    scan = storage.scan_partition(j, d)
+    got = Crc32c.calculate_batch(d, scan["app_offset"].astype(np.int64),
+                                 scan["app_length"].astype(np.int32))
+    assert [int(x) for x in np.asarray(got).view(np.uint32)] == \
+        [oracle.crc32c(d[int(o):int(o) + int(n)].tobytes())
+         for o, n in zip(scan["app_offset"], scan["app_length"])]
+    live = [i for i, n in enumerate(scan["app_length"]) if n > 0]
+    victims = live[1::3]
+    d2 = d.copy()
+    for i in victims:
+        d2[int(scan["app_offset"][i]) + int(scan["app_length"][i]) // 2] ^= 0x10
+    res = storage.verify_partition(j, d2)
+    assert res["n_bad"] == len(victims)
+    assert res["bad_record_offsets"].tolist() == scan["record_offset"][victims].tolist()
 
 
 def test_verify_detects_exact_corruptions(cuda):
@@ -30,12 +66,12 @@ def test_verify_detects_exact_corruptions(cuda):
     j, d = storage.write_partition(apps)
     res = storage.verify_partition(j, d)
     assert res["n_bad"] == 0 and res["n_messages"] == len(apps)
-    scan = storage.scan_partition(j, d)
+    scan = storage.scan_partition(j, d)  # backward journal order
     # flip one byte in the payload of some messages, and one stored CRC
     victims = sorted(set(int(i) for i in rng.integers(0, len(apps), size=37)
-                         if sizes[int(i)] > 0))
+                         if scan["app_length"][int(i)] > 0))
     for i in victims:
-        o = int(scan["app_offset"][i]) + int(rng.integers(0, sizes[i]))
+        o = int(scan["app_offset"][i]) + int(rng.integers(0, int(scan["app_length"][i])))
         d[o] ^= 0x01
     jcrc_victim = next(i for i in range(len(apps)) if i not in victims)
     rec = int(scan["record_offset"][jcrc_victim])
@@ -44,7 +80,7 @@ def test_verify_detects_exact_corruptions(cuda):
     want = scan["record_offset"][sorted(victims + [jcrc_victim])]
     assert res2["n_bad"] == len(want)
     assert res2["bad_record_offsets"].tolist() == want.tolist()
-    # bounded report: the first bad_cap offsets, full count
+    # bounded report: the first bad_cap alarms, full count
     res3 = storage.verify_partition(j, d, bad_cap=5)
     assert res3["n_bad"] == len(want) and res3["bad_record_offsets"].tolist() == want[:5].tolist()
 

@@ -75,22 +75,23 @@ def _fixture():
 def test_partition_scan_fixture(golden):
     j, d = _fixture()
     s = storage.scan_partition(j, d)
-    assert s["record_offset"].tolist() == golden["journal_file"]["message_record_offsets"]
-    assert s["crc32c"].tolist() == golden["journal_file"]["crc"]
-    assert s["app_offset"].tolist() == [52, 76] and s["app_length"].tolist() == [11, 11]
+    assert s["recovery_rc"] == 0
+    assert s["record_offset"].tolist() == golden["recovery"]["outstanding_record_offsets"]
+    assert s["crc32c"].tolist() == golden["journal_file"]["crc"][1:]
+    assert s["app_offset"].tolist() == [76] and s["app_length"].tolist() == [11]
 
 
-def test_partition_scan_matches_numpy_walk():
+def test_partition_scan_matches_restatement():
     rng = np.random.default_rng(2)
     sizes = list(range(20)) + list(rng.integers(0, 40000, size=500))
     apps = [rng.integers(0, 256, size=int(n), dtype=np.uint8).tobytes() for n in sizes]
     j, d = storage.write_partition(apps)
     s = storage.scan_partition(j, d)
-    r = storage.journal_message_records(j)
-    off, ln = storage.data_app_ranges(d, r["data_offset"])
-    assert s["record_offset"].tolist() == r["record_offset"].tolist()
-    assert s["app_offset"].tolist() == off.tolist() and s["app_length"].tolist() == ln.tolist()
-    assert s["crc32c"].tolist() == r["crc32c"].tolist() == [oracle.crc32c(a) for a in apps]
+    r = storage.recovery_selection_py(j, d)
+    assert s["record_offset"].tolist() == r["record_offset"]
+    assert s["app_offset"].tolist() == r["app_offset"]
+    assert s["app_length"].tolist() == r["app_length"]
+    assert s["crc32c"].tolist()[::-1] == [oracle.crc32c(a) for a in apps]
     # zero-filled (pre-allocated) journal tail ends the walk
     jz = np.concatenate([j, np.zeros(60 * 7, np.uint8)])
     assert storage.scan_partition(jz, d)["record_offset"].size == len(apps)
@@ -99,23 +100,34 @@ def test_partition_scan_matches_numpy_walk():
 @pytest.mark.parametrize("mutate", ["jmagic", "dmagic", "rec_magic", "beyond", "padding",
                                     "zero_words"])
 def test_partition_scan_rejects_malformed(mutate):
+    """File-level damage is a format error; damage to a record is the
+    reference's recovery rc (the walk stops at a record with a bad magic)."""
     j, d = storage.write_partition([b"hello world", b"x" * 77])
     j, d = j.copy(), d.copy()
-    rec0 = storage.scan_partition(j, d)["record_offset"][0]
+    rec0 = int(storage.scan_partition(j, d)["record_offset"][-1])  # "hello world"
+    want = None
     if mutate == "jmagic":
         j[0] ^= 1
     elif mutate == "dmagic":
         d[4] ^= 1
     elif mutate == "rec_magic":
-        j[int(rec0) + 57] ^= 1
+        j[rec0 + 57] ^= 1
+        want = (0, 0, 0)  # journal bounded before it: nothing to recover
     elif mutate == "beyond":
-        j[int(rec0) + 32:int(rec0) + 36] = np.frombuffer((10**6).to_bytes(4, "big"), np.uint8)
+        j[rec0 + 32:rec0 + 36] = np.frombuffer((10**6).to_bytes(4, "big"), np.uint8)
+        want = (storage.RC_INVALID_DATA_OFFSET, rec0, 1)
     elif mutate == "padding":
         d[40 + 12 + 11] = 9   # "hello world" record: 12 B header + 11 B + 1 pad byte
+        want = (storage.RC_INVALID_DATA_RECORD, rec0, 1)
     elif mutate == "zero_words":
         d[40:44] = 0
-    with pytest.raises(storage.StorageFormatError):
-        storage.scan_partition(j, d)
+        want = (storage.RC_INVALID_DATA_RECORD, rec0, 1)
+    if want is None:
+        with pytest.raises(storage.StorageFormatError):
+            storage.scan_partition(j, d)
+        return
+    s = storage.scan_partition(j, d)
+    assert (s["recovery_rc"], s["error_record_offset"], s["record_offset"].size) == want
 
 
 KEY = b"\x11\x22\x33\x44\x55"
@@ -189,6 +201,9 @@ def test_gpu_only_walks_refuse_without_device():
     with pytest.raises(N.BmqCrcError) as e:
         storage.verify_partition(j, d)
     assert e.value.rc == N.BMQCRC_ENODEV
+    # a partition whose selection is empty needs no device
+    w = storage.PartitionWriter()
+    assert storage.verify_partition(*w.files())["n_messages"] == 0
     b = PutEventBuilder(defer_crc=True)
     b.pack_message(b"payload")
     with pytest.raises(N.BmqCrcError) as e:

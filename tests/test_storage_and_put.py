@@ -19,24 +19,33 @@ def _fixture():
             np.fromfile(os.path.join(GOLD, "test.bmq_data"), np.uint8))
 
 
-def test_fixture_journal_records(golden):
+def test_fixture_recovery_selection(golden):
+    """bmqstoragetool's fixture: two MESSAGE records, the first confirmed and
+    deleted (DELETION at 404), so recovery CRCs only the outstanding one
+    (summary_result.txt: 1 outstanding; test_journalfile.py TEST_GUID_1)."""
     j, d = _fixture()
-    r = storage.journal_message_records(j)
-    assert r["record_offset"].tolist() == golden["journal_file"]["message_record_offsets"]
-    assert r["crc32c"].tolist() == golden["journal_file"]["crc"]
-    assert r["data_offset"].tolist() == [40, 64]
-    off, ln = storage.data_app_ranges(d, r["data_offset"])
-    assert off.tolist() == [52, 76] and ln.tolist() == [11, 11]
-    for o, l, c in zip(off, ln, r["crc32c"]):
-        assert oracle.crc32c(d[int(o):int(o) + int(l)].tobytes()) == int(c)
+    rec = golden["recovery"]
+    py = storage.recovery_selection_py(j, d)
+    assert py["recovery_rc"] == 0
+    assert py["record_offset"] == rec["outstanding_record_offsets"]
+    assert len(py["record_offset"]) == rec["outstanding_messages"]
+    guid = bytes.fromhex(rec["outstanding_guids"][0])
+    r = int(py["record_offset"][0])
+    assert j[r + 36:r + 52].tobytes() == guid
+    assert py["crc32c"] == golden["journal_file"]["crc"][1:]
+    o, n = py["app_offset"][0], py["app_length"][0]
+    assert d[o:o + n].tobytes() == b"hello world"
+    assert oracle.crc32c(d[o:o + n].tobytes()) == py["crc32c"][0]
+    assert storage.journal_bounds_py(j) == (rec["last_valid_syncpoint_offset"],
+                                            rec["last_valid_record_offset"])
 
 
 def test_writer_reproduces_data_fixture():
     _, d = _fixture()
     j2, d2 = storage.write_partition([b"hello world", b"hello world"])
     assert np.array_equal(d2, d)
-    r = storage.journal_message_records(j2)
-    assert r["crc32c"].tolist() == [3381945770, 3381945770]
+    r = storage.recovery_selection_py(j2, d2)
+    assert r["crc32c"] == [3381945770, 3381945770]
 
 
 def test_writer_roundtrip_random():
@@ -44,37 +53,28 @@ def test_writer_roundtrip_random():
     apps = [rng.integers(0, 256, size=int(n), dtype=np.uint8).tobytes()
             for n in rng.integers(0, 3000, size=200)]
     j, d = storage.write_partition(apps)
-    r = storage.journal_message_records(j)
-    off, ln = storage.data_app_ranges(d, r["data_offset"])
-    assert [d[int(o):int(o) + int(l)].tobytes() for o, l in zip(off, ln)] == apps
-    assert r["crc32c"].tolist() == [oracle.crc32c(a) for a in apps]
+    r = storage.recovery_selection_py(j, d)
+    got = [d[o:o + n].tobytes() for o, n in zip(r["app_offset"], r["app_length"])]
+    assert got[::-1] == apps  # backward journal order
+    assert r["crc32c"][::-1] == [oracle.crc32c(a) for a in apps]
 
 
 def test_preallocated_journal_tail_is_ignored():
-    j, _ = storage.write_partition([b"a", b"bc"])
+    j, d = storage.write_partition([b"a", b"bc"])
     jz = np.concatenate([j, np.zeros(600, np.uint8)])
-    assert storage.journal_message_records(jz)["crc32c"].size == 2
+    assert len(storage.recovery_selection_py(jz, d)["crc32c"]) == 2
 
 
-@pytest.mark.parametrize("corrupt", ["magic", "padding", "header_words", "type"])
+@pytest.mark.parametrize("corrupt", ["magic", "type"])
 def test_invalid_files_raise(corrupt):
     j, d = storage.write_partition([b"hello world"])
     if corrupt == "magic":
         j[0] ^= 0xFF
         with pytest.raises(storage.StorageFormatError):
-            storage.journal_message_records(j)
-        return
-    if corrupt == "type":
-        with pytest.raises(storage.StorageFormatError):
-            storage.journal_message_records(d)  # a DATA file is not a journal
-        return
-    r = storage.journal_message_records(j)
-    if corrupt == "padding":
-        d[-1] = 0
+            storage.recovery_selection_py(j, d)
     else:
-        d[40] &= 0x1F  # headerWords = 0
-    with pytest.raises(storage.StorageFormatError):
-        storage.data_app_ranges(d, r["data_offset"])
+        with pytest.raises(storage.StorageFormatError):
+            storage.recovery_selection_py(d, d)  # a DATA file is not a journal
 
 
 def test_put_event_layout_and_roundtrip():

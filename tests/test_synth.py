@@ -15,8 +15,9 @@ def test_partition_matches_writer():
     assert np.array_equal(journal, jw)
     assert np.array_equal(data, dw)
     walk = S.scan_partition(journal, data)
-    assert np.array_equal(walk["app_offset"], app_off)
-    assert np.array_equal(walk["app_length"], app_len)
+    assert walk["recovery_rc"] == 0
+    assert np.array_equal(walk["app_offset"][::-1], app_off)
+    assert np.array_equal(walk["app_length"][::-1], app_len)
 
 
 def test_put_event_matches_builder():

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """k_fold time vs segment size and blocks per CU for a few batch shapes (GPU
-box), one JSON line per point.  Explicit seg_bytes; BMQCRC_TUNE bit1 / bit3
-force 1 / 2 blocks per CU in a child process per grid choice."""
+box), one JSON line per point.  Explicit seg_bytes; the grid is forced to 1 / 2
+blocks per CU by the variant builds variant_bpc1.so / variant_bpc2.so
+(tools/build_variant.sh bpc1 -DBMQCRC_TUNE_BITS=2; bpc2 -DBMQCRC_TUNE_BITS=8),
+swapped in as libbmqcrc.so for a child process per grid choice."""
 import json
 import os
 import subprocess
@@ -45,16 +47,22 @@ if __name__ == "__main__":
         n, size, seg = map(int, sys.argv[1:4])
         print(child(n, size, seg))
         sys.exit(0)
+    import shutil
+    lib = os.path.join(ROOT, "blazingmq_amd", "lib")
+    base = os.path.join("/tmp", "shape_sweep_base.so")
+    shutil.copy(os.path.join(lib, "libbmqcrc.so"), base)
     for n, size in SHAPES:
-        for tune in (2, 8):
+        for bpc in (1, 2):
+            shutil.copy(os.path.join(lib, "variant_bpc%d.so" % bpc), os.path.join(lib, "libbmqcrc.so"))
             for seg in SEGS:
-                env = dict(os.environ, BMQCRC_TUNE=str(tune))
                 r = subprocess.run([sys.executable, __file__, str(n), str(size), str(seg)],
-                                   capture_output=True, text=True, env=env, timeout=120)
+                                   capture_output=True, text=True, timeout=120)
                 if r.returncode != 0:
+                    shutil.copy(base, os.path.join(lib, "libbmqcrc.so"))
                     print(json.dumps({"n": n, "size": size, "seg": seg, "error": r.stderr[-300:]}))
                     sys.exit(1)
                 us = float(r.stdout.strip().splitlines()[-1])
-                print(json.dumps({"n": n, "size": size, "blocks_per_cu": 1 if tune == 2 else 2,
+                print(json.dumps({"n": n, "size": size, "blocks_per_cu": bpc,
                                   "seg": seg or "auto", "k_fold_us": round(us, 2),
                                   "TBps": round(n * size / us / 1e6, 3)}), flush=True)
+    shutil.copy(base, os.path.join(lib, "libbmqcrc.so"))
