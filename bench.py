@@ -4,10 +4,17 @@
 Metric and configs: BASELINE.json.  A "step" is one bmqcrc_crc32c_batch call
 (planner kernels + fold kernel) over one resident batch.  Default workload
 (N=1) is configs[2]: 65,536 messages x 64 KiB of synthetic random payload
-(splitmix64 stream, seed 2) -- the headline HBM-bound regime.  With
---gpus N (torchrun, one process per GPU) every rank CRCs its own 64k x 64 KiB
-slice of an N-times larger batch (weak scaling, no data-path collective; a
-gloo barrier brackets the timed region and the time is the max over ranks).
+(splitmix64 stream, seed 2) -- the headline HBM-bound regime.
+
+--gpus N runs one process per GPU.  Under torchrun (WORLD_SIZE set) it must
+equal WORLD_SIZE; without it, bench.py starts `torch.distributed.run
+--nproc-per-node N` itself as a child process (before touching a GPU) and
+exits with its status.  Every rank CRCs its own 64k x 64 KiB slice of an
+N-times larger batch (weak scaling, no data-path collective; a gloo barrier
+brackets the timed region and the time is the max over ranks).  For N > 1
+the line also carries "strong_scaling": BASELINE configs[3] (Zipf 4M, one
+batch split byte-balanced over the N ranks) timed across the ranks and, in
+the same run, the whole batch on rank 0's GPU alone -- the measured speed-up.
 
 Output: one JSON line on rank 0 (see README/DESIGN.md for fields).
 """
@@ -104,6 +111,11 @@ def parse():
                         "verify, deferred PUT-event CRCs, Blob batches, ledger validation")
     p.add_argument("--e2e", action="store_true",
                    help="end-to-end mode: H2D from pinned host + CRC + D2H (for DESIGN.md)")
+    p.add_argument("--no-strong-scaling", action="store_true",
+                   help="N > 1: skip the strong-scaled Zipf object")
+    p.add_argument("--launch-check", action="store_true",
+                   help="test hook: start the ranks, rendezvous over gloo and print the "
+                        "world as rank 0 sees it, without touching a GPU")
     a = p.parse_args()
     a.config_given = a.config is not None
     if a.config is None:
@@ -122,13 +134,24 @@ def cpu_model():
     return platform.processor()
 
 
+def host_threads():
+    """This GPU's share of the host: the box's thread allotment
+    (OMP_NUM_THREADS, 16 per GPU on the pool), else min(nproc, 16)."""
+    try:
+        return max(1, int(os.environ["OMP_NUM_THREADS"]))
+    except (KeyError, ValueError):
+        return min(os.cpu_count() or 1, 16)
+
+
 def cpu_baseline(lens_np, seed, seconds):
     """Reference-equivalent CPU CRC32C (oracle, SSE4.2 3-way; BDE 4.39 is not
     available offline) on a bounded sample (first ~256 MiB of messages) of the
-    same synthetic workload, on up to 16 host threads (this GPU's CPU share)."""
+    same synthetic workload: single thread (the reference's own methodology,
+    bmqp_crc32c.t.cpp:1116-1120) and this GPU's share of the host's threads
+    (the test5 pattern, one thread per core over message slices)."""
     import numpy as np
     import oracle
-    threads = min(os.cpu_count() or 1, 16)
+    threads = host_threads()
     csum = np.cumsum(lens_np, dtype=np.uint64)
     n = max(1, int(np.searchsorted(csum, 256 << 20, side="right")))
     lens = np.ascontiguousarray(lens_np[:n])
@@ -147,9 +170,12 @@ def cpu_baseline(lens_np, seed, seconds):
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
+        "single_thread_value": round(gib / t1, 3),
         "sample": "first %d msgs (%.0f MiB) of the same synthetic batch, %d passes on %d "
-                  "threads; SSE4.2 crc32q 3-way interleaved (bdlde::Crc32c default analogue, "
-                  "oracle/crc32c_oracle.c); single-thread %.2f GiB/s; host %s, nproc %d"
+                  "threads (this GPU's share of the host: OMP_NUM_THREADS, 16 per GPU on the "
+                  "pool; the whole host is not ours to load); SSE4.2 crc32q 3-way interleaved "
+                  "(bdlde::Crc32c default analogue, oracle/crc32c_oracle.c); single-thread "
+                  "%.2f GiB/s; host %s, nproc %d"
                   % (n, gib * 1024, reps, threads, gib / t1, cpu_model(), os.cpu_count()),
     }
 
@@ -169,7 +195,7 @@ def cpu_table(args):
 
     import numpy as np
     import oracle
-    threads = min(os.cpu_count() or 1, 16)
+    threads = host_threads()
     configs = [args.config] if args.config_given else list(CONFIGS)
     for cfg in configs:
         _, gen, seed, _ = CONFIGS[cfg]
@@ -225,7 +251,7 @@ def protocol(args):
 
     from blazingmq_amd import _native as N
     from blazingmq_amd import csl, put_event, storage, synth
-    threads = min(os.cpu_count() or 1, 16)
+    threads = host_threads()
     reps = max(3, args.steps // 4)
 
     def cpu_leg(buf, offs, lens, walk_s):
@@ -365,10 +391,56 @@ def pmc_traffic(config):
     return int(s["traffic_bytes_per_launch"]), os.path.relpath(paths[-1], ROOT)
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def spawn_ranks(args):
+    """--gpus N without torchrun: run N ranks under torch.distributed.run as a
+    child process (this process has not touched a GPU) and return its status."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1",
+           "--nproc-per-node", str(args.gpus), "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
+def launch_check(args, world, rank):
+    """The rank plumbing of a GPU run (rendezvous, barrier, max over ranks)
+    with no GPU: rank 0 prints what it sees."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+        dist.barrier()
+        t = torch.tensor([float(rank)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        top = int(t[0])
+        dist.destroy_process_group()
+    else:
+        top = 0
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "max_rank": top,
+                          "gpus_arg": args.gpus}), flush=True)
+    return 0
+
+
 def main():
     args = parse()
     if args.cpu_table:
         return cpu_table(args)
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        return spawn_ranks(args)
+    world = int(world_env or "1")
+    if world != args.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world), file=sys.stderr)
+        return 2
+    if args.launch_check:
+        return launch_check(args, world, int(os.environ.get("RANK", "0")))
     if args.protocol:
         import torch
         torch.cuda.set_device(0)
@@ -380,13 +452,14 @@ def main():
     import blazingmq_amd as bmq
     from blazingmq_amd import Crc32c
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo")
     # BENCH_DEVICE pins every rank to one GPU: only for rehearsing the
-    # multi-process path on a one-GPU box (never used for reported numbers).
+    # multi-process path on a one-GPU box.  Such a line is marked
+    # "rehearsal_single_gpu" and reports n_gpus 1, never a scaling point.
+    rehearsal = "BENCH_DEVICE" in os.environ
     local = int(os.environ.get("BENCH_DEVICE", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -459,6 +532,7 @@ def main():
             step(True)
         torch.cuda.synchronize(dev)
     kern_ms, kern_cnt = bmq.kernel_timing(local, stream)
+    del arena  # the strong-scaling leg below needs the memory
     bytes_all = total_bytes
     kern_max = kern_ms / max(kern_cnt, 1)
     if world > 1:
@@ -490,6 +564,10 @@ def main():
         bt = torch.tensor([bad, checked], dtype=torch.int64)
         dist.all_reduce(bt)
         bad, checked = int(bt[0]), int(bt[1])
+    strong = None
+    if world > 1 and not args.no_strong_scaling and not args.config_given:
+        strong = strong_scaling(args, bmq, Crc32c, dev, stream, world, rank, dist)
+        bad += strong.pop("_bad")
 
     if rank == 0:
         value = bytes_all / 2**30 * args.steps / elapsed
@@ -501,7 +579,7 @@ def main():
             "metric": "device-resident CRC32C GiB/s over batched payloads, 1/2/4/8 MI355X",
             "value": round(value, 2),
             "unit": "GiB/s",
-            "n_gpus": world,
+            "n_gpus": 1 if rehearsal else world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 4),
@@ -522,12 +600,91 @@ def main():
                          "alg_bytes_per_launch": alg_bytes},
             "parity": {"checked_msgs": checked, "mismatches": bad},
         }
+        if rehearsal:
+            res["rehearsal_single_gpu"] = True
+            res["ranks_on_one_gpu"] = world
+        if strong is not None:
+            res["strong_scaling"] = strong
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(lens_np, seed, args.cpu_seconds)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
     return 1 if bad else 0
+
+
+def strong_scaling(args, bmq, Crc32c, dev, stream, world, rank, dist):
+    """BASELINE configs[3] strong-scaled: the Zipf 4M
+    batch split byte-balanced over the `world` ranks (no collective), K steps
+    timed like the main line (barriers, max over ranks); then, in the same
+    run, the whole batch on rank 0's GPU alone (the N=1 time) while the other
+    ranks wait.  speedup = t(1 GPU) / t(N GPUs); targets >= 3.5x at 4, >= 7x
+    at 8.  A sampled parity check of both legs against the oracle."""
+    import numpy as np
+    import oracle
+    import torch
+    _, gen, seed, _ = CONFIGS["zipf_4M"]
+
+    def leg(lens_np, begin, active):
+        n = int(lens_np.size)
+        offs_np = np.zeros(n, dtype=np.int64)
+        if n > 1:
+            np.cumsum(lens_np[:-1], dtype=np.int64, out=offs_np[1:])
+        total = int(lens_np.sum(dtype=np.uint64))
+        elapsed, bad = 0.0, 0
+        if active:
+            arena = torch.empty(max(total, 8), dtype=torch.uint8, device=dev)
+            _fill_slice(bmq, arena, seed, begin)
+            offsets = torch.from_numpy(offs_np).to(dev)
+            lengths = torch.from_numpy(lens_np.view(np.int32)).to(dev)
+            out = torch.empty(n, dtype=torch.int32, device=dev)
+
+            def step():
+                Crc32c.calculate_batch(arena, offsets, lengths, None, out, stream=stream,
+                                       sync=False)
+            t_settle = time.perf_counter()
+            while time.perf_counter() - t_settle < args.settle_seconds / 2:
+                step()
+                torch.cuda.synchronize(dev)
+            for _ in range(args.warmup):
+                step()
+            torch.cuda.synchronize(dev)
+        dist.barrier()
+        if active:
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                step()
+            torch.cuda.synchronize(dev)
+            elapsed = time.perf_counter() - t0
+        dist.barrier()
+        if active:
+            got = out.cpu().numpy().view(np.uint32)
+            rng = np.random.default_rng(100 + rank)
+            for i in np.unique(np.concatenate([[0, n - 1], rng.integers(0, n, size=62)])):
+                exp = oracle.crc32c(oracle.fill_payload(begin + int(offs_np[i]), int(lens_np[i]),
+                                                        seed), 0, "hw")
+                bad += int(got[i] != exp)
+            del arena, offsets, lengths, out
+            torch.cuda.empty_cache()
+        t = torch.tensor([elapsed, bad, total], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        tb = torch.tensor([total], dtype=torch.int64)
+        dist.all_reduce(tb)
+        return float(t[0]), int(t[1]), int(tb[0])
+
+    lens_r, begin_r = gen(rank, world)
+    t_n, bad_n, bytes_n = leg(lens_r, begin_r, True)
+    lens_1, begin_1 = gen(0, 1) if rank == 0 else (np.zeros(1, np.uint32), 0)
+    t_1, bad_1, _ = leg(lens_1, begin_1, rank == 0)
+    gib = bytes_n / 2**30 * args.steps
+    return {"config": "zipf_4M: " + CONFIGS["zipf_4M"][0], "scaling": "strong",
+            "value": round(gib / t_n, 2), "unit": "GiB/s", "n_gpus": world,
+            "ms_per_step": round(1e3 * t_n / args.steps, 4),
+            "one_gpu_value": round(gib / t_1, 2),
+            "one_gpu_ms_per_step": round(1e3 * t_1 / args.steps, 4),
+            "speedup": round(t_1 / t_n, 3), "payload_bytes_total": bytes_n,
+            "one_gpu_leg": "the whole batch on rank 0's GPU in the same run",
+            "_bad": bad_n + bad_1}
 
 
 def e2e(args, dev, stream, arena_dev, offs_np, lens_np, total_bytes, world, rank, dist, desc):

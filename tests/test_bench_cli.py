@@ -35,3 +35,26 @@ def test_cpu_table_runs_without_gpu():
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert {d["variant"] for d in lines} == {"hw", "hw_serial", "sw"}
     assert all(d["config"] == "1k_x_4KiB" and d["GiBps"] > 0 for d in lines)
+
+
+def test_gpus_n_spawns_its_own_ranks():
+    """`bench.py --gpus 2` without torchrun starts two ranks itself (a child
+    torch.distributed.run, no exec) that rendezvous over gloo; rank 0 sees a
+    world of 2.  --launch-check stops before any GPU call."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--launch-check"], capture_output=True, text=True, timeout=300,
+                       cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    assert lines[0]["n_gpus"] == 2 and lines[0]["max_rank"] == 1 and lines[0]["gpus_arg"] == 2
+
+
+def test_gpus_must_match_world_size():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4",
+                        "--launch-check"], capture_output=True, text=True, timeout=120,
+                       cwd=ROOT, env=env)
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
