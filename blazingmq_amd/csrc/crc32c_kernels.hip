@@ -509,8 +509,15 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* excl, uint3
 // block replaces a grid-wide arrival counter and a dependent last-block pass
 // at the end of k_plan.
 struct PlanTotals {
-    uint32_t total, identity, uni;
+    uint32_t total, identity, uni, overflow;
 };
+
+// Segment indices are 32-bit.  A batch of overlapping messages can hold more
+// segments than that (4,096 messages of 2^32-1 bytes at 256-byte segments is
+// 6.9e10); k_plan flags a block whose count passes kSegLimit and the consumers
+// then fold every message whole in one lane (BMQCRC_F_WHOLE_MESSAGES'
+// schedule: correct for any lengths, just slower), never a wrapped count.
+constexpr uint64_t kSegLimit = 0xFFFFFF00ull;
 
 // The loads are split from the reduction so that k_fold can issue them
 // together with its other prologue loads.
@@ -534,6 +541,7 @@ __device__ PlanTotals plan_reduce(const BatchArgs& a, PlanLds* pl, const PlanWor
     const uint32_t j = threadIdx.x, nb = a.nblocks;
     const uint32_t v = w.v, nn = w.nn, u = w.u, u0 = w.u0;
     PlanTotals t;
+    t.overflow = 0u;
     // Closed forms need no offsets: one barrier for identity, two for uniform.
     const int ragged = __syncthreads_or(nn != 0u);
     if (!ragged) {  // every message exactly one segment
@@ -542,9 +550,30 @@ __device__ PlanTotals plan_reduce(const BatchArgs& a, PlanLds* pl, const PlanWor
         t.uni = 1u;
         return t;
     }
+    // a block over the limit (k_plan stores ~0 segments), or a sum past it
+    // (<= 256 blocks: the 64-bit sum of the words cannot wrap)
+    uint64_t s64 = v;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        s64 += shfl64(s64, (int)((threadIdx.x & 63u) ^ (uint32_t)o));
+    }
+    if ((threadIdx.x & 63u) == 0) {
+        pl->wsum[threadIdx.x >> 6] = (uint32_t)min(s64, (uint64_t)0xffffffffu);
+    }
+    __syncthreads();
+    uint64_t all = 0;
+    for (uint32_t wv = 0; wv < (blockDim.x >> 6); ++wv) {
+        all += pl->wsum[wv];
+    }
     const int mismatch = __syncthreads_or(u != u0);
     t.identity = 0u;
     t.uni = (!mismatch && u0 != 0xffffffffu && u0 != 0u) ? u0 : 0u;
+    if (all > kSegLimit || (t.uni && (uint64_t)a.n * t.uni > kSegLimit)) {
+        t.overflow = 1u;
+        t.uni = 0u;
+        t.total = (uint32_t)a.n;
+        return t;
+    }
     if (t.uni) {
         t.total = (uint32_t)a.n * t.uni;
         return t;
@@ -676,11 +705,16 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     // BMQCRC_F_WHOLE_MESSAGES: segment g = message g, one segment each, no
     // planner ran.  Otherwise the batch totals come from k_plan's block words.
     __shared__ PlanLds pl;
-    PlanTotals pt = {(uint32_t)a.n, 1u, 0u};
+    PlanTotals pt = {(uint32_t)a.n, 1u, 0u, 0u};
     if (!whole) {
         pt = plan_reduce(a, &pl, pw);
     } else {
         __syncthreads();
+    }
+    // more segments than 32-bit indices hold: every message in one lane
+    const uint32_t wholef = whole | pt.overflow;
+    if (pt.overflow) {
+        pt.identity = 1u;
     }
     const uint32_t total = pt.total;
     const uint32_t identity = pt.identity;
@@ -688,7 +722,7 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     // the size-class order exists only if the histogram and k_plan_sort ran
     // (and seginfo could hold every segment)
     const uint32_t sorted =
-        (whole || !a.map_planned || identity || uni || total > a.max_segs) ? 0u : 1u;
+        (wholef || !a.map_planned || identity || uni || total > a.max_segs) ? 0u : 1u;
     const uint32_t ngroups = (total + 63u) / 64u;
     const uint32_t SEG = a.seg_bytes;
     const uint64_t arena = (uint64_t)(uintptr_t)a.arena;
@@ -738,7 +772,7 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         const uint64_t off = cur.off;
         const uint32_t nseg =
             !valid ? 0u
-                   : (whole ? 1u : (seg_shift ? ((len - 1u) >> seg_shift) : (len - 1u) / SEG) + 1u);
+                   : (wholef ? 1u : (seg_shift ? ((len - 1u) >> seg_shift) : (len - 1u) / SEG) + 1u);
         const uint64_t mstart = arena + off;
         const uint64_t mend = mstart + len;
         const SegGeom geo = seg_geom(mstart, len, k, nseg, SEG);
@@ -931,11 +965,13 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
     __shared__ uint32_t wsum[40];
     __shared__ uint32_t sh[4];
     __shared__ uint32_t hist[kBuckets];
+    __shared__ unsigned long long segs64;  // the block's segments without wrapping
     constexpr bool classes = CLASSES;  // a ragged batch is expected: size-class histogram
     if (threadIdx.x == 0) {
         sh[1] = 0;            // messages with != 1 segment
         sh[2] = 0xffffffffu;  // min segments per message
         sh[3] = 0;            // max segments per message
+        segs64 = 0;
     }
     if (threadIdx.x < kBuckets) {
         hist[threadIdx.x] = 0;
@@ -966,6 +1002,7 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
     // uniform block consumers compute it (seg_first_g).
     const bool one_tile = hi - lo <= kTile;
     uint32_t carry = 0, mn = 0xffffffffu, mx = 0, non1 = 0;
+    uint64_t mine64 = 0;  // this thread's segments (u32 tile scans may wrap: see kSegLimit)
     uint32_t ns[kPlanV], run0 = 0;
     for (uint64_t base = lo; base < hi; base += kTile) {
         uint32_t L[kPlanV];
@@ -1013,6 +1050,7 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
             }
             sum += ns[v];
         }
+        mine64 += sum;
         uint32_t excl;
         const uint32_t tot = block_scan(sum, &excl, wsum);
         run0 = carry + excl;
@@ -1042,10 +1080,15 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
             full += (uint32_t)__shfl_xor((int)full, o);
         }
     }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mine64 += shfl64(mine64, lane ^ o);
+    }
     if ((threadIdx.x & 63) == 0) {
         atomicMin(&sh[2], mn);
         atomicMax(&sh[3], mx);
         atomicAdd(&sh[1], non1);
+        atomicAdd(&segs64, (unsigned long long)mine64);
         if (full) {
             atomicAdd(&hist[size_class(seg >> 7)], full);
         }
@@ -1066,7 +1109,7 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
         }
     }
     if (threadIdx.x == 0) {  // read by the next launches (kernel boundary: plain stores)
-        a.block_sum[blockIdx.x] = carry;
+        a.block_sum[blockIdx.x] = segs64 > kSegLimit ? 0xffffffffu : carry;
         a.block_sum[a.nblocks + blockIdx.x] = sh[1];
         a.block_sum[2u * a.nblocks + blockIdx.x] = sh[2] == sh[3] ? sh[2] : 0xffffffffu;
     }
@@ -1105,8 +1148,8 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_sort(BatchArgs a)
     __shared__ uint32_t part[2][kPlanBlock / kBuckets][kBuckets];
     __shared__ PlanLds pl;
     const PlanTotals pt = plan_totals(a, &pl);
-    if (pt.identity || pt.uni || pt.total > a.max_segs) {
-        return;  // closed form, or more segments than seginfo holds (k_fold searches)
+    if (pt.identity || pt.uni || pt.overflow || pt.total > a.max_segs) {
+        return;  // closed form, overflow, or more segments than seginfo holds (k_fold searches)
     }
     const int lane = threadIdx.x & 63;
     // This block's slice of every bucket, from k_plan's per-block histograms
