@@ -273,6 +273,18 @@ int open_ctx(int dev, void* user_stream, Ctx* c)
     return 0;
 }
 
+// A speculative single launch (BatchArgs::spec) is used only when every
+// k_fold wave owns at least one group of 64 messages: a message longer than
+// one segment is then folded by the wave that met it, and no wave is idle
+// while another folds one.
+bool spec_eligible(const Ctx& c, uint64_t n, uint32_t blocks_per_cu)
+{
+    const uint32_t per_cu = (kTuneBits & 2u) ? 1u : (kTuneBits & 8u) ? 2u : blocks_per_cu;
+    const uint64_t waves = (uint64_t)(c.st->num_cus > 0 ? c.st->num_cus : 256) * per_cu *
+                           kWavesPerBlock;
+    return (n + 63) / 64 >= waves;
+}
+
 // Enqueue planner + fold on device pointers (caller holds c.w->mu).
 // Segment size (when the caller left it at 0) and k_fold blocks per CU, from
 // the batch's average message size and total bytes.  Measured on MI355X
@@ -332,9 +344,14 @@ int run_batch(Ctx& c, uint32_t flags, uint32_t seg, const void* arena, uint64_t 
         a.max_segs = n;
     } else if ((rc = plan_ws(w, n, arena_bytes, seg, &a))) {
         return rc;
-    } else if (!(kTuneBits & 16u) &&
-               __atomic_load_n(w->hint_host, __ATOMIC_RELAXED) == kHintClosed) {
-        a.map_planned = 0;  // last batch was closed-form: predict this one is too
+    } else if (!(kTuneBits & 16u)) {
+        const uint32_t hint = __atomic_load_n(w->hint_host, __ATOMIC_RELAXED);
+        if (hint == kHintClosed || hint == kHintIdentity) {
+            a.map_planned = 0;  // last batch was closed-form: predict this one is too
+        }
+        if (hint == kHintIdentity && spec_eligible(c, n, a.blocks_per_cu)) {
+            a.spec = 1;  // ... and one segment per message: one launch, no planner
+        }
     }
     a.arena = (const uint8_t*)arena;
     a.offsets = offsets;

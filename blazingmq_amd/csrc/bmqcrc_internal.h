@@ -52,13 +52,21 @@ struct BatchArgs {
                                //    runs before k_fold; 0: skipped (the previous batch on this
                                //    workspace was closed-form) and a ragged batch maps segments
                                //    by binary search instead -- slower, never wrong
-    uint32_t* shape_hint;      // host-mapped word or nullptr: k_fold writes kHintClosed or
-                               // kHintRagged, the host reads it when planning the next batch
+    uint32_t* shape_hint;      // host-mapped word or nullptr: k_fold writes kHintIdentity,
+                               // kHintClosed or kHintRagged, the host reads it when planning
+                               // the next batch
+    // Speculative single launch (spec = 1): the previous batch on this
+    // workspace had one segment per message, so no planner runs and k_fold
+    // folds message g in lane g.  A message longer than one segment is
+    // skipped there and folded by the same wave afterwards, 64 segments at a
+    // time -- correct for any batch, only slower when the guess was wrong.
+    uint32_t spec;
 };
 
 constexpr uint32_t kHintUnknown = 0;
-constexpr uint32_t kHintClosed = 1;  // identity or uniform segment counts
+constexpr uint32_t kHintClosed = 1;  // uniform segment counts (> 1)
 constexpr uint32_t kHintRagged = 2;
+constexpr uint32_t kHintIdentity = 3;  // one segment per message
 
 }  // namespace bmqcrc
 

@@ -261,29 +261,34 @@ __device__ __forceinline__ uint32_t tab_lookup(uint32_t tab_lds, int k, uint32_t
     return *(const lds_u32*)(uintptr_t)(tab_lds + k * 1024u + b * 4u);
 }
 
-__device__ __forceinline__ uint32_t tail_round(const uint32_t (&q)[32], const uint32_t (&p)[32],
-                                               const uint32_t (&m)[32], uint32_t tab_lds)
+// FIRST: the stream is this one round (zero history), so every tap into the
+// previous round reads zero and is dropped at compile time -- no ring to
+// clear for one-line streams.
+template <bool FIRST>
+__device__ __forceinline__ void tail_rem(const uint32_t (&q)[32], const uint32_t (&p)[32],
+                                         const uint32_t (&m)[32], uint32_t (&R)[32])
 {
     // R_d = m_d ^ (taps that stay in the previous round: d + k <= 31); a pair
     // (k, k+1) with d + k + 1 <= 31 is p[d + k]
-    uint32_t R[32];
 #pragma unroll
     for (int d = 0; d < 32; ++d) {
         uint32_t t[20];
         int nt = 0;
         t[nt++] = m[d];
+        if (!FIRST) {
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            if (d + kSingles[i] <= 31) {
-                t[nt++] = q[d + kSingles[i]];
+            for (int i = 0; i < 3; ++i) {
+                if (d + kSingles[i] <= 31) {
+                    t[nt++] = q[d + kSingles[i]];
+                }
             }
-        }
 #pragma unroll
-        for (int i = 0; i < 7; ++i) {
-            if (d + kPairs[i] + 1 <= 31) {
-                t[nt++] = p[d + kPairs[i]];
-            } else if (d + kPairs[i] <= 31) {
-                t[nt++] = q[d + kPairs[i]];
+            for (int i = 0; i < 7; ++i) {
+                if (d + kPairs[i] + 1 <= 31) {
+                    t[nt++] = p[d + kPairs[i]];
+                } else if (d + kPairs[i] <= 31) {
+                    t[nt++] = q[d + kPairs[i]];
+                }
             }
         }
         uint32_t acc = t[0];
@@ -297,6 +302,10 @@ __device__ __forceinline__ uint32_t tail_round(const uint32_t (&q)[32], const ui
         }
         R[d] = acc;
     }
+}
+
+__device__ __forceinline__ uint32_t tail_horner(const uint32_t (&R)[32], uint32_t tab_lds)
+{
     uint32_t c = 0;
 #pragma unroll
     for (int d = 0; d < 32; d += 2) {
@@ -680,8 +689,9 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         tw[i] = c_ty[t >> 8][t & 255u];
     }
     const uint32_t whole = a.whole;
+    const uint32_t spec_mode = a.spec;  // speculative single launch: no planner ran
     PlanWords pw = {0u, 0u, 0u, 0u};
-    if (!whole) {
+    if (!whole && !spec_mode) {
         pw = plan_load(a);
     }
     // x^(-8p) un-shift table -> LDS too: a per-lane index, so from constant
@@ -702,11 +712,12 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         xneg8[threadIdx.x] = xn;
     }
 
-    // BMQCRC_F_WHOLE_MESSAGES: segment g = message g, one segment each, no
-    // planner ran.  Otherwise the batch totals come from k_plan's block words.
+    // BMQCRC_F_WHOLE_MESSAGES and speculative launches: group g = messages
+    // 64g..64g+63, no planner ran.  Otherwise the batch totals come from
+    // k_plan's block words.
     __shared__ PlanLds pl;
     PlanTotals pt = {(uint32_t)a.n, 1u, 0u, 0u};
-    if (!whole) {
+    if (!whole && !spec_mode) {
         pt = plan_reduce(a, &pl, pw);
     } else {
         __syncthreads();
@@ -726,9 +737,13 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     const uint32_t ngroups = (total + 63u) / 64u;
     const uint32_t SEG = a.seg_bytes;
     const uint64_t arena = (uint64_t)(uintptr_t)a.arena;
-    if (a.shape_hint && blockIdx.x == 0 && threadIdx.x == 0 && !whole) {
-        // batch shape for the host's next launch decision (host-mapped word)
-        __hip_atomic_store(a.shape_hint, (identity || uni) ? kHintClosed : kHintRagged,
+    if (a.shape_hint && blockIdx.x == 0 && threadIdx.x == 0 && !whole && !spec_mode) {
+        // batch shape for the host's next launch decision (host-mapped word);
+        // a speculative launch keeps kHintIdentity unless a message is queued
+        __hip_atomic_store(a.shape_hint,
+                           (identity && !pt.overflow) ? kHintIdentity
+                                                      : (uni || pt.overflow) ? kHintClosed
+                                                                             : kHintRagged,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 
@@ -737,113 +752,104 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
 
     const uint32_t stride = gridDim.x * kWavesPerBlock;
     const uint32_t seg_shift = (SEG & (SEG - 1u)) == 0 ? (uint32_t)__builtin_ctz(SEG) : 0u;
-    // Descriptor pipeline across groups: the (message, part) of the group
-    // after next and the (offset, length, seed) of the next group are loaded
-    // while the current group folds, so no group starts on a cold load.
-    uint32_t g = g0;
-    SegDesc nxt = {0ull, 0u, 0u, 0u, 0u};
-    SegRef ref2 = {0u, 0u};
-    if (g < ngroups) {
-        const uint32_t s0 = g * 64u + (uint32_t)lane;
-        if (identity) {  // whole or identity: the speculative descriptors are the ones
-            nxt = spec;
-        } else {
-            nxt = fetch_desc(a, map_segment(a, &pl, s0, s0 < total, identity, uni, sorted),
-                             s0 < total);
-        }
-        const uint32_t s1 = (g + stride) * 64u + (uint32_t)lane;
-        ref2 = map_segment(a, &pl, s1, g + stride < ngroups && s1 < total, identity, uni,
-                           sorted);
-    }
-    for (; g < ngroups; g += stride) {
-        // ---------------------------------------------------- descriptor
-        const uint32_t seg = g * 64u + (uint32_t)lane;
-        const bool valid = seg < total;
-        const SegDesc cur = nxt;
-        {
-            const uint32_t s1 = (g + stride) * 64u + (uint32_t)lane;
-            const bool v1 = g + stride < ngroups && s1 < total;
-            nxt = fetch_desc(a, ref2, v1);
-            const uint32_t s2 = (g + 2u * stride) * 64u + (uint32_t)lane;
-            ref2 = map_segment(a, &pl, s2, g + 2u * stride < ngroups && s2 < total, identity,
-                               uni, sorted);
-        }
-        const uint32_t msg = cur.msg, k = cur.k, len = cur.len, seed = cur.seed;
-        const uint64_t off = cur.off;
-        const uint32_t nseg =
-            !valid ? 0u
-                   : (wholef ? 1u : (seg_shift ? ((len - 1u) >> seg_shift) : (len - 1u) / SEG) + 1u);
-        const uint64_t mstart = arena + off;
-        const uint64_t mend = mstart + len;
-        const SegGeom geo = seg_geom(mstart, len, k, nseg, SEG);
-        const uint64_t E = geo.E, L0 = geo.L0;
-        const bool first = valid && k == 0;
-        const uint32_t nl = valid ? geo.nl : 0u;
-        const uint32_t R = wave_max(nl);  // lane 0 always holds a valid segment here: R >= 1
-        // right-aligned stream: this lane's line j is round r0 + j
-        const uint32_t r0 = R - nl;
-        const uint32_t sl = valid ? (uint32_t)(geo.S - L0) : 0u;  // S's offset in line 0
-        const uint64_t el = valid ? E - L0 : 0u;                  // E's offset in the stream
-        const bool lo_part = (sl & 15u) != 0;
-        const bool hi_part = (el & 15u) != 0;
-        const uint32_t jE = (uint32_t)(el >> 7);    // line holding E's cut piece
-        const uint32_t eE = (uint32_t)(el & 127u);  // E's offset in that line
 
-        // ------------------------------------------ DMA source per instruction
-        // pieces [gS, gE) of the stream overlap [S, E); the stream piece index
-        // in round r is 8 (r - r0) + piece
-        const uint32_t gS = sl >> 4;
-        const uint32_t gE = (uint32_t)((el + 15u) >> 4);
-        const uint32_t plo_l = 8u * r0 + gS;
-        const uint32_t pcnt_l = valid ? gE - gS : 0u;
-        const uint64_t pb_l = L0 - ((uint64_t)r0 << 7);
+    // One group = 64 segments, one per lane.  Its per-lane geometry and the
+    // DMA source of every instruction of its rounds (see dma_round).
+    struct Group {
         uint64_t pbase[8];
         uint32_t plo[8], pcnt[8];
+        uint64_t E, L0, mend;
+        uint32_t msg, k, nseg, nl, R, r0, sl, jE, eE, c0;
+        bool valid, first, lo_part, hi_part;
+    };
+    // Geometry of one lane's segment k of a message of nseg segments.
+    auto setup_lane = [&](bool valid, uint32_t msg, uint32_t k, uint32_t nseg, uint64_t off,
+                          uint32_t len, uint32_t seed, Group& G) {
+        G.valid = valid;
+        G.msg = msg;
+        G.k = k;
+        G.nseg = valid ? nseg : 0u;
+        const uint64_t mstart = arena + off;
+        G.mend = mstart + len;
+        const SegGeom geo = seg_geom(mstart, len, G.k, G.nseg, SEG);
+        G.E = geo.E;
+        G.L0 = geo.L0;
+        G.first = G.valid && G.k == 0;
+        G.nl = G.valid ? geo.nl : 0u;
+        // every lane invalid (a speculative group of queued messages): one
+        // round of zeros, nothing stored
+        G.R = max(wave_max(G.nl), 1u);
+        // right-aligned stream: this lane's line j is round r0 + j
+        G.r0 = G.R - G.nl;
+        G.sl = G.valid ? (uint32_t)(geo.S - G.L0) : 0u;  // S's offset in line 0
+        const uint64_t el = G.valid ? G.E - G.L0 : 0u;   // E's offset in the stream
+        G.lo_part = (G.sl & 15u) != 0;
+        G.hi_part = (el & 15u) != 0;
+        G.jE = (uint32_t)(el >> 7);    // line holding E's cut piece
+        G.eE = (uint32_t)(el & 127u);  // E's offset in that line
+        G.c0 = ~seed;
+        // DMA source per instruction: pieces [gS, gE) of the stream overlap
+        // [S, E); the stream piece index in round r is 8 (r - r0) + piece
+        const uint32_t gS = G.sl >> 4;
+        const uint32_t gE = (uint32_t)((el + 15u) >> 4);
+        const uint32_t plo_l = 8u * G.r0 + gS;
+        const uint32_t pcnt_l = G.valid ? gE - gS : 0u;
+        const uint64_t pb_l = G.L0 - ((uint64_t)G.r0 << 7);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int src = 8 * i + (lane >> 3);
             const uint32_t pp = ((uint32_t)lane & 7u) ^ ((4u * i + ((uint32_t)lane >> 4)) & 7u);
-            pbase[i] = shfl64(pb_l, src) + 16u * pp;
-            plo[i] = (uint32_t)__shfl((int)plo_l, src) - pp;
-            pcnt[i] = (uint32_t)__shfl((int)pcnt_l, src);
+            G.pbase[i] = shfl64(pb_l, src) + 16u * pp;
+            G.plo[i] = (uint32_t)__shfl((int)plo_l, src) - pp;
+            G.pcnt[i] = (uint32_t)__shfl((int)pcnt_l, src);
         }
+    };
+    auto segments = [&](uint32_t len) {
+        return len ? (seg_shift ? ((len - 1u) >> seg_shift) : (len - 1u) / SEG) + 1u : 0u;
+    };
+    bool long_seen = false;  // speculative: a message of this wave needs the second pass
+    // The segment of group gg in this lane (planned or speculative mapping).
+    auto setup = [&](const SegDesc& d, uint32_t gg, Group& G) {
+        const uint32_t seg = gg * 64u + (uint32_t)lane;
+        bool valid = seg < total;
+        uint32_t nseg = !valid ? 0u : (wholef ? 1u : segments(d.len));
+        if (spec_mode) {
+            // a message longer than one segment is left to the wave's second
+            // pass (below); an empty message is folded whole (its seed)
+            long_seen |= __ballot(valid && nseg > 1u) != 0;
+            valid = valid && nseg <= 1u;
+            nseg = 1u;
+        }
+        setup_lane(valid, d.msg, d.k, nseg, d.off, d.len, d.seed, G);
+    };
+    auto issue_first_rounds = [&](const Group& G) {
+        dma_round<NT>(wave_lds, G.pbase, G.plo, G.pcnt, zero, 0);
+        if (G.R > 1) {
+            dma_round<NT>(wave_lds + kSlotBytes, G.pbase, G.plo, G.pcnt, zero, 1);
+        }
+    };
 
-        // ------------------------------------------------------ fold rounds
+    // Rounds of a group whose first two rounds are in flight: rounds 0 .. R-2
+    // fold into the ring; the last round (peeled, so no remainder array is
+    // carried through the loop) gives the remainder words Rm.
+    auto fold_rounds = [&](const Group& G, uint32_t (&Rm)[32]) {
         uint32_t q[32], p[32];
-#pragma unroll
-        for (int d = 0; d < 32; ++d) {
-            q[d] = 0;
-            p[d] = 0;
-        }
-        uint32_t crc = 0;
-        const uint32_t c0 = ~seed;
-
-        dma_round<NT>(wave_lds, pbase, plo, pcnt, zero, 0);
-        if (R > 1) {
-            dma_round<NT>(wave_lds + kSlotBytes, pbase, plo, pcnt, zero, 1);
-        }
-        for (uint32_t r = 0; r < R; ++r) {
-            const uint32_t slot = wave_lds + (r & 1u) * kSlotBytes;
-            if (r + 1 < R) {
-                asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
+        const uint32_t R = G.R;
+        auto load_line = [&](uint32_t r, uint32_t slot, uint32_t (&m)[32]) {
             // Byte edges of this round's line: the piece cut by S (first line),
             // the piece cut by E, and the seed word (first segment only; it may
             // spill into the second line).  Lanes before their stream (j wraps)
             // match none of these.
-            const uint32_t j = r - r0;
-            const bool fx_lo = lo_part && j == 0u;
-            const bool fx_hi = hi_part && j == jE;
-            const bool fx_sd = first && (j == 0u || (j == 1u && sl > 124u));
+            const uint32_t j = r - G.r0;
+            const bool fx_lo = G.lo_part && j == 0u;
+            const bool fx_hi = G.hi_part && j == G.jE;
+            const bool fx_sd = G.first && (j == 0u || (j == 1u && G.sl > 124u));
             if (__ballot(fx_lo || fx_hi || fx_sd)) {
                 if (fx_lo || fx_hi || fx_sd) {
-                    line_fixup(slot, rd_off, fx_lo, sl, fx_hi, eE, fx_sd, (int)(sl - 128u * j),
-                               c0);
+                    line_fixup(slot, rd_off, fx_lo, G.sl, fx_hi, G.eE, fx_sd,
+                               (int)(G.sl - 128u * j), G.c0);
                 }
             }
-            uint32_t m[32];
 #pragma unroll
             for (int kk = 0; kk < 8; ++kk) {
                 const u32x4 v = *(lds_cu4*)(uintptr_t)(slot + (rd_off ^ (16u * kk)));
@@ -852,51 +858,67 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
                 m[4 * kk + 2] = v.z;
                 m[4 * kk + 3] = v.w;
             }
+        };
+        for (uint32_t r = 0; r + 1 < R; ++r) {
+            const uint32_t slot = wave_lds + (r & 1u) * kSlotBytes;
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            uint32_t m[32];
+            load_line(r, slot, m);
             if (r + 2 < R) {
-                dma_round<NT>(slot, pbase, plo, pcnt, zero, r + 2);
+                dma_round<NT>(slot, G.pbase, G.plo, G.pcnt, zero, r + 2);
             }
-            if (r + 1 < R) {
-                if (r == 0) {
-                    first_round(q, p, m);
-                } else {
-                    fold_round(q, p, m);
-                }
+            if (r == 0) {
+                first_round(q, p, m);
             } else {
-                crc = tail_round(q, p, m, tab_lds);  // every lane's last line: one tail per wave
+                fold_round(q, p, m);
             }
         }
+        const uint32_t slot = wave_lds + ((R - 1u) & 1u) * kSlotBytes;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        uint32_t m[32];
+        load_line(R - 1u, slot, m);
+        if (R == 1) {
+            tail_rem<true>(q, p, m, Rm);  // one-line streams: no history
+        } else {
+            tail_rem<false>(q, p, m, Rm);  // every lane's last line: one tail per wave
+        }
+    };
 
-        // ------------------------------------------------ move + combine
-        // raw(stream) = raw(segment) * x^(8 padE): un-shift the zero padding
-        // (table x^-8p + one 160-VALU multiply), then move the segment to the
-        // message end with x^(8 after) (sparse exponent: bits no lane needs are
-        // skipped wave-uniformly).
+    // Move + combine of a folded group: raw(stream) = raw(segment) * x^(8
+    // padE): un-shift the zero padding (table x^-8p + one 160-VALU multiply),
+    // then move the segment to the message end with x^(8 after) (sparse
+    // exponent: bits no lane needs are skipped wave-uniformly).
+    auto contribution = [&](const Group& C, uint32_t crc) {
         uint32_t contrib = 0;
-        const uint32_t padE = valid ? (uint32_t)(L0 + ((uint64_t)nl << 7) - E) : 0u;
+        const uint32_t padE = C.valid ? (uint32_t)(C.L0 + ((uint64_t)C.nl << 7) - C.E) : 0u;
         if (__ballot(padE != 0) == 0) {
-            contrib = valid ? crc : 0u;
-        } else if (valid) {
+            contrib = C.valid ? crc : 0u;
+        } else if (C.valid) {
             contrib = gmul(crc, xneg8[padE]);
         }
-        const uint32_t e_after = valid ? mersenne31(8ull * (mend - E)) : 0u;
+        const uint32_t e_after = C.valid ? mersenne31(8ull * (C.mend - C.E)) : 0u;
         contrib = mul_xpow(contrib, e_after);
-        if (first) {
+        if (C.first) {
             contrib ^= 0xffffffffu;
         }
+        return contrib;
+    };
+    auto finish = [&](const Group& C, uint32_t crc) {
+        uint32_t contrib = contribution(C, crc);
         // XOR-reduce each run of adjacent lanes holding the same message, then
         // one store or atomic per run: the run head owns the result.  A
         // message may occupy several runs of one wave (the size-class sort
         // can split its segments across a bucket boundary inside the wave),
         // so runs are delimited by a head ballot, never by key equality, and
         // a head stores plainly only when its run is the whole message.
-        if (__ballot(valid && nseg != 1u) == 0) {
+        if (__ballot(C.valid && C.nseg != 1u) == 0) {
             // every segment of this group is a whole message: no runs to combine
-            if (valid) {
-                a.out[msg] = contrib;
+            if (C.valid) {
+                a.out[C.msg] = contrib;
             }
-            continue;
+            return;
         }
-        const uint32_t key = valid ? msg : 0xffffffffu;
+        const uint32_t key = C.valid ? C.msg : 0xffffffffu;
         const uint32_t pkey = (uint32_t)__shfl_up((int)key, 1);
         const bool head = lane == 0 || pkey != key;
         const uint64_t heads = __ballot(head);
@@ -910,13 +932,105 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
                 contrib ^= ov;
             }
         }
-        if (valid && head) {
-            if (k == 0 && rend - (uint32_t)lane == nseg) {
-                a.out[msg] = contrib;  // the whole message is this run
+        if (C.valid && head) {
+            if (C.k == 0 && rend - (uint32_t)lane == C.nseg) {
+                a.out[C.msg] = contrib;  // the whole message is this run
             } else {
-                atomicXor(&a.out[msg], contrib);
+                atomicXor(&a.out[C.msg], contrib);
             }
         }
+    };
+
+    // Speculative launches only: the wave's messages longer than one segment,
+    // skipped by its first pass, folded with all 64 lanes (lane l: segment
+    // 64c + l of chunk c), one message at a time; the chunks' contributions
+    // are XOR-accumulated in registers and stored once.  A wave never waits
+    // on another, and in the predicted case (every message one segment) no
+    // wave runs this pass.
+    auto second_pass = [&]() {
+        bool any = false;
+        for (uint32_t gg = g0; gg < ngroups; gg += stride) {
+            const uint32_t i = gg * 64u + (uint32_t)lane;
+            const uint32_t len = i < a.n ? a.lengths[i] : 0u;
+            uint64_t todo = __ballot(segments(len) > 1u);
+            any = any || todo != 0;
+            for (; todo; todo &= todo - 1ull) {
+                const uint32_t msg = gg * 64u + (uint32_t)__builtin_ctzll(todo);
+                const uint64_t off = a.offsets[msg];
+                const uint32_t mlen = a.lengths[msg];
+                const uint32_t seed = a.seeds ? a.seeds[msg] : 0u;
+                const uint32_t nseg = segments(mlen);
+                uint32_t acc = 0;
+                for (uint32_t c = 0; 64u * c < nseg; ++c) {
+                    const uint32_t k = 64u * c + (uint32_t)lane;
+                    Group H;
+                    setup_lane(k < nseg, msg, k, nseg, off, mlen, seed, H);
+                    issue_first_rounds(H);
+                    uint32_t Rm[32];
+                    fold_rounds(H, Rm);
+                    uint32_t x = contribution(H, tail_horner(Rm, tab_lds));
+#pragma unroll
+                    for (int o = 32; o > 0; o >>= 1) {
+                        x ^= (uint32_t)__shfl_xor((int)x, o);
+                    }
+                    acc ^= x;
+                }
+                if (lane == 0) {
+                    a.out[msg] = acc;
+                }
+            }
+        }
+        if (any && lane == 0 && a.shape_hint) {  // mispredicted: plan the next batch
+            __hip_atomic_store(a.shape_hint, kHintRagged, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    };
+
+    // Descriptor pipeline: the (offset, length, seed) of the next group and
+    // the (message, part) of the one after are loaded a group ahead, and a
+    // group's first two rounds are in flight before the previous group's
+    // remainder reduction, move and combine run -- a wave's LDS slots are
+    // never idle while it computes.
+    uint32_t g = g0;
+    Group G;
+    SegDesc nxt = {0ull, 0u, 0u, 0u, 0u};
+    SegRef ref2 = {0u, 0u};
+    if (g < ngroups) {
+        const uint32_t s0 = g * 64u + (uint32_t)lane;
+        const SegDesc d0 =
+            identity ? spec
+                     : fetch_desc(a, map_segment(a, &pl, s0, s0 < total, identity, uni, sorted),
+                                  s0 < total);
+        const uint32_t s1 = (g + stride) * 64u + (uint32_t)lane;
+        const bool v1 = g + stride < ngroups && s1 < total;
+        nxt = fetch_desc(a, map_segment(a, &pl, s1, v1, identity, uni, sorted), v1);
+        const uint32_t s2 = (g + 2u * stride) * 64u + (uint32_t)lane;
+        ref2 = map_segment(a, &pl, s2, g + 2u * stride < ngroups && s2 < total, identity, uni,
+                           sorted);
+        setup(d0, g, G);
+        issue_first_rounds(G);
+    }
+    for (; g < ngroups; g += stride) {
+        uint32_t Rm[32];
+        fold_rounds(G, Rm);
+        // The slots are read: the next group's first rounds go out now, so
+        // they load while this group's remainder is reduced and combined.
+        const Group C = G;
+        if (g + stride < ngroups) {
+            const SegDesc d = nxt;
+            const uint32_t s2 = (g + 2u * stride) * 64u + (uint32_t)lane;
+            const bool v2 = g + 2u * stride < ngroups && s2 < total;
+            nxt = fetch_desc(a, ref2, v2);
+            const uint32_t s3 = (g + 3u * stride) * 64u + (uint32_t)lane;
+            ref2 = map_segment(a, &pl, s3, g + 3u * stride < ngroups && s3 < total, identity, uni,
+                               sorted);
+            setup(d, g + stride, G);
+            issue_first_rounds(G);
+        }
+        finish(C, tail_horner(Rm, tab_lds));
+    }
+    if (spec_mode && long_seen) {
+        second_pass();
     }
 }
 
@@ -1422,7 +1536,7 @@ extern "C" int bmqcrc_launch_batch(const BatchArgs* a, void* stream, int num_cus
     if (a->n == 0) {
         return 0;
     }
-    if (!a->whole) {
+    if (!a->whole && !a->spec) {
         if (a->map_planned) {
             hipLaunchKernelGGL(k_plan<true>, dim3(a->nblocks), dim3(kPlanBlock), 0, s, *a);
         } else {

@@ -434,3 +434,48 @@ def test_batch_leaves_current_device_unchanged(cuda):
                                           ctypes.byref(o)))
         assert torch.cuda.current_device() == dev_before
     assert out.tolist() == [oracle.crc32c(a[:4000].tobytes()), oracle.crc32c(a[100:103].tobytes())]
+
+
+def test_speculative_single_launch(cuda):
+    """After a batch of one segment per message, the next batch on the same
+    stream runs as ONE k_fold launch with no planner (BatchArgs::spec): lane
+    g folds message g, and a message longer than one segment is queued and
+    folded in chunks of 64 segments by the waves still running.  Every batch
+    of a sequence that mispredicts in every way -- long messages scattered
+    among short ones (including the last group), all messages long (one
+    chunk each), messages of thousands of segments (many chunks XOR into one
+    out word), empty messages, seeds -- is bit-exact against the oracle."""
+    import torch
+    rng = np.random.default_rng(78)
+    arena_np = rng.integers(0, 256, size=48 << 20, dtype=np.uint8)
+    arena = torch.from_numpy(arena_np).to(cuda)
+    s = torch.cuda.Stream(cuda)
+    n = 300_000  # >= 64 messages for every k_fold wave: eligible
+
+    def run(lens, tag):
+        lens = np.asarray(lens, np.uint32)
+        offs = np.array(rng.integers(0, arena_np.size - lens.astype(np.int64) + 1), np.int64)
+        seeds = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64).astype(np.uint32)
+        seeds[::3] = 0
+        got = Crc32c.calculate_batch(arena, torch.from_numpy(offs).to(cuda),
+                                     torch.from_numpy(lens.view(np.int32)).to(cuda),
+                                     torch.from_numpy(seeds.view(np.int32)).to(cuda),
+                                     stream=s)
+        s.synchronize()
+        exp = oracle.batch(arena_np, offs, lens, seeds, nthreads=8)
+        bad = np.nonzero(got.cpu().numpy().view(np.uint32) != exp)[0]
+        assert bad.size == 0, (tag, [(int(i), int(lens[i])) for i in bad[:8]])
+
+    short = lambda: rng.integers(0, 257, size=n)  # noqa: E731  one segment at every auto shape
+    scattered = short()
+    where = np.concatenate([rng.integers(0, n, size=60), np.arange(n - 40, n)])
+    scattered[where] = rng.integers(300, 300_000, size=where.size)
+    scattered[-1] = 5 << 20  # thousands of segments, in the very last group
+    all_long = np.full(n, 2000)
+    for tag, lens in (("identity", short()), ("spec identity", short()),
+                      ("spec scattered", scattered), ("planned after", short()),
+                      ("spec again", short()), ("spec all long", all_long),
+                      ("planned", short()), ("spec empties", np.where(
+                          rng.integers(0, 4, size=n) == 0, 0, short())),
+                      ("spec", short())):
+        run(lens, tag)
