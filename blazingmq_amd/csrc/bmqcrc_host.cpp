@@ -288,15 +288,17 @@ bool spec_eligible(const Ctx& c, uint64_t n, uint32_t blocks_per_cu)
 // Enqueue planner + fold on device pointers (caller holds c.w->mu).
 // Segment size (when the caller left it at 0) and k_fold blocks per CU, from
 // the batch's average message size and total bytes.  Measured on MI355X
-// (profiles/r01/sweeps/shape_sweep*.jsonl):
+// (profiles/r01/sweeps/, profiles/r02/seg_sweep_*.jsonl):
 //  * >= 4 GiB of >= 16 KiB messages: 64 KiB segments, one 4-wave block per CU
 //    (64k x 64 KiB: 620 us, the fastest shape);
-//  * otherwise two blocks per CU, and 16 KiB segments when that still gives
-//    every wave slot a group of 64 (Zipf 4M, 2 GiB of 64 KiB messages);
-//  * smaller batches: the longest of 2 KiB, 1 KiB, 512 B, 256 B that gives
-//    every wave two groups, so each wave streams steadily: 256 MiB of 64 KiB
-//    messages 72 -> 56 us, 1k x 4 KiB 36 -> 13 us.  4 and 8 KiB segments
-//    measured 10-30 % slower than both 2 and 16 KiB at every size tried.
+//  * otherwise two blocks per CU; messages averaging >= 16 KiB get 16 KiB
+//    segments when that still gives every wave slot a group of 64 (2 GiB of
+//    64 KiB messages);
+//  * everything else: the longest of 2 KiB, 1 KiB, 512 B, 256 B that gives
+//    every wave two groups.  Segments of 4 and 8 KiB are never chosen: a wave
+//    whose 64 segments start 4 or 8 KiB apart (uniform messages of those
+//    sizes) streams at 0.71-0.75 of the roofline against 0.83-0.84 with
+//    2 KiB segments, and Zipf 4M is within 2 % at 2, 4 and 16 KiB.
 void auto_shape(uint64_t n, uint64_t arena_bytes, int num_cus, uint32_t* seg,
                 uint32_t* blocks_per_cu)
 {
@@ -313,7 +315,7 @@ void auto_shape(uint64_t n, uint64_t arena_bytes, int num_cus, uint32_t* seg,
     *blocks_per_cu = 2;
     if (*seg == 0) {
         const uint64_t slots = cus * 2 * wave_segs;
-        if (arena_bytes / kDefaultSegBytes >= slots) {
+        if (large && arena_bytes / kDefaultSegBytes >= slots) {
             *seg = kDefaultSegBytes;
             return;
         }
@@ -327,9 +329,20 @@ void auto_shape(uint64_t n, uint64_t arena_bytes, int num_cus, uint32_t* seg,
     }
 }
 
+uint64_t max_length(const uint32_t* lengths, uint64_t n)
+{
+    uint32_t m = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        m = std::max(m, lengths[i]);
+    }
+    return m;
+}
+
+// host_max_len: the longest message when the lengths were seen on the host
+// (host-buffer calls), UINT64_MAX when they live on the device.
 int run_batch(Ctx& c, uint32_t flags, uint32_t seg, const void* arena, uint64_t arena_bytes,
               const uint64_t* offsets, const uint32_t* lengths, const uint32_t* seeds,
-              uint32_t* out, uint64_t n)
+              uint32_t* out, uint64_t n, uint64_t host_max_len = UINT64_MAX)
 {
     Workspace* w = c.w;
     BatchArgs a;
@@ -352,6 +365,9 @@ int run_batch(Ctx& c, uint32_t flags, uint32_t seg, const void* arena, uint64_t 
         if (hint == kHintIdentity && spec_eligible(c, n, a.blocks_per_cu)) {
             a.spec = 1;  // ... and one segment per message: one launch, no planner
         }
+    }
+    if (!a.whole && host_max_len <= a.seg_bytes) {
+        a.spec = 1;  // known, not guessed: every message is one segment
     }
     a.arena = (const uint8_t*)arena;
     a.offsets = offsets;
@@ -421,7 +437,8 @@ int batch_one(int dev, void* user_stream, uint32_t flags, uint32_t seg, const vo
     }
     if ((rc = run_batch(c, flags, seg, w->arena.p, arena_bytes, (const uint64_t*)w->offsets.p,
                         (const uint32_t*)w->lengths.p,
-                        seeds ? (const uint32_t*)w->seeds.p : nullptr, (uint32_t*)w->out.p, n))) {
+                        seeds ? (const uint32_t*)w->seeds.p : nullptr, (uint32_t*)w->out.p, n,
+                        max_length(lengths, n)))) {
         return rc;
     }
     HIP_TRY(hipMemcpyAsync(out, w->out.p, 4 * n, hipMemcpyDeviceToHost, c.s));
@@ -610,7 +627,8 @@ int verify_locked(Ctx& c, Workspace* w, const bmqcrc_opts& o, uint32_t seg, bool
         d_exp = (const uint32_t*)w->expected.p;
     }
     if ((rc = run_batch(c, o.flags, seg, d_arena, arena_bytes, d_off, d_len, nullptr,
-                        (uint32_t*)w->out.p, n))) {
+                        (uint32_t*)w->out.p, n,
+                        dev_ptrs ? UINT64_MAX : max_length(lengths, n)))) {
         return rc;
     }
     HIP_TRY(hipMemsetAsync(w->vcount.p, 0, 4, c.s));
@@ -751,7 +769,7 @@ int bmqcrc_verify_host_overlapped(const void* arena, uint64_t arena_bytes,
         }
         if ((rc = run_batch(c, o.flags, seg, w->arena.p, arena_bytes,
                             (const uint64_t*)w->offsets.p, (const uint32_t*)w->lengths.p, nullptr,
-                            (uint32_t*)w->out.p, n))) {
+                            (uint32_t*)w->out.p, n, max_length(len, n)))) {
             return rc;
         }
         HIP_TRY(hipMemcpyAsync(crcs->data(), w->out.p, 4 * n, hipMemcpyDeviceToHost, c.s));
@@ -830,7 +848,8 @@ int bmqcrc_crc32c_blobs(const void* arena, uint64_t arena_bytes, const uint64_t*
         d_out = (uint32_t*)w->out.p;
     }
     if (nbuf && (rc = run_batch(c, o.flags, seg, d_arena, arena_bytes, d_off, d_len, nullptr,
-                                (uint32_t*)w->buf_crc.p, nbuf))) {
+                                (uint32_t*)w->buf_crc.p, nbuf,
+                                dev_ptrs ? UINT64_MAX : max_length(buf_lengths, nbuf)))) {
         return rc;
     }
     if (bmqcrc_launch_blob_combine((const uint32_t*)w->buf_crc.p, d_len, d_first, d_seeds, d_out,
