@@ -304,7 +304,17 @@ int walk_recovery(const uint8_t* j, uint64_t jlen, const uint8_t* d, uint64_t dl
         res->error_record = pos;
         return 0;
     };
-    auto live = [&](uint64_t key) { return qv->keys.count(key) != 0; };
+    // Partitions hold few queues and a walk meets the same key in long runs:
+    // remember the last answer instead of hashing every record.
+    uint64_t live_key = ~0ull;
+    bool live_ans = false;
+    auto live = [&](uint64_t key) {
+        if (key != live_key) {
+            live_key = key;
+            live_ans = qv->keys.count(key) != 0;
+        }
+        return live_ans;
+    };
 
     // ---- first pass (:1120-1453): deleted queues, queues alive without CSL,
     // the first sync point's offset.
@@ -353,7 +363,7 @@ int walk_recovery(const uint8_t* j, uint64_t jlen, const uint8_t* d, uint64_t dl
                 if (live(qkey)) {  // a CREATION met earlier backwards: two live queues
                     return fail_at(BMQCRC_RECOVERY_DUPLICATE_QUEUE_KEY, pos);
                 }
-            } else if (!qv->keys.insert(qkey).second) {
+            } else if (live_key = ~0ull, !qv->keys.insert(qkey).second) {
                 return fail_at(BMQCRC_RECOVERY_DUPLICATE_QUEUE_KEY, pos);
             }
         }
@@ -367,6 +377,9 @@ int walk_recovery(const uint8_t* j, uint64_t jlen, const uint8_t* d, uint64_t dl
     uint32_t lease = head.lease;
     uint64_t seq = head.seq + 1;
     auto before_queue_deletion = [&](uint64_t qkey, uint64_t pos) {
+        if (deleted_queue.empty()) {
+            return false;
+        }
         auto it = deleted_queue.find(qkey);
         return it != deleted_queue.end() && pos < it->second;
     };
@@ -445,13 +458,16 @@ int walk_recovery(const uint8_t* j, uint64_t jlen, const uint8_t* d, uint64_t dl
             if (o == 0 || o > dlen) {
                 return fail_at(BMQCRC_RECOVERY_INVALID_DATA_OFFSET, pos);
             }
-            if (before_queue_deletion(qkey, pos) || purged_queues.count(qkey)) {
+            if (before_queue_deletion(qkey, pos) ||
+                (!purged_queues.empty() && purged_queues.count(qkey))) {
                 continue;  // the DATA file is never touched for these (:2390-2393)
             }
-            auto del = deleted_guids.find(g);
-            if (del != deleted_guids.end()) {
-                deleted_guids.erase(del);
-                continue;
+            if (!deleted_guids.empty()) {
+                auto del = deleted_guids.find(g);
+                if (del != deleted_guids.end()) {
+                    deleted_guids.erase(del);
+                    continue;
+                }
             }
             // DATA record checks (:2494-2575).  Where the reference would read
             // past the end of the DATA file, the record is invalid here.
