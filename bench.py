@@ -354,7 +354,29 @@ def protocol(args):
     line("blobs_device", "bmqp::Crc32c::calculate(const bdlbb::Blob&) per blob "
          "(bmqp_crc32c.cpp:47-67)", nblob, total, gpu_s, 0.0, cpu_leg(host, bo, bl, 0.0), parity,
          "device-resident buffers: per-buffer CRCs + on-device combine, one synchronous call")
-    del arena, host
+
+    # 3b. the same blobs with their buffers scattered in host memory (each a
+    #     separate allocation, like a broker's 4 KiB blob buffers):
+    #     Crc32c::calculateBatch(const Blob*) -> bmqcrc_crc32c_gather (pinned
+    #     staging ring, gather overlapped with the H2D copies, one fold launch)
+    hbufs = [np.array(host[i * bsz:(i + 1) * bsz]) for i in range(nblob * nbuf)]
+    ptrs = (ctypes.c_void_p * len(hbufs))(*[b.ctypes.data for b in hbufs])
+    hlen = np.full(len(hbufs), bsz, np.uint32)
+    hfirst = np.arange(nblob + 1, dtype=np.uint64) * nbuf
+    hout = np.zeros(nblob, np.uint32)
+    hopts = N.make_opts()
+
+    def gather():
+        N.check(N.lib.bmqcrc_crc32c_gather(ptrs, hlen.ctypes.data, len(hbufs), hfirst.ctypes.data,
+                                           None, hout.ctypes.data, nblob, ctypes.byref(hopts)))
+    gpu_s = _wall(gather, reps)
+    parity = {"equal": bool(np.array_equal(hout, exp))}
+    line("blobs_host_gather", "bmqp::Crc32c::calculate(const bdlbb::Blob&) per blob "
+         "(bmqp_crc32c.cpp:47-67)", nblob, total, gpu_s, 0.0, cpu_leg(host, bo, bl, 0.0), parity,
+         "host buffers (one allocation each) gathered through the pinned ring and copied to HBM "
+         "by %d threads, one fold launch, D2H of the CRCs; CPU leg on a contiguous copy" %
+         min(8, (total + (4 << 20) - 1) // (4 << 20)))
+    del arena, host, hbufs
 
     # 4. cluster state ledger validation (mqbc_clusterstateledgerutil.cpp:248-336)
     r = 32768

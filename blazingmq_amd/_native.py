@@ -30,7 +30,8 @@ class BmqCrcError(RuntimeError):
 class Opts(ctypes.Structure):
     _fields_ = [("struct_size", ctypes.c_uint32), ("device", ctypes.c_int32),
                 ("stream", ctypes.c_void_p), ("flags", ctypes.c_uint32),
-                ("seg_bytes", ctypes.c_uint32)]
+                ("seg_bytes", ctypes.c_uint32), ("ndevices", ctypes.c_uint32),
+                ("devices", ctypes.c_void_p)]
 
 
 # One HIP runtime per process: when PyTorch-ROCm is present it ships its own
@@ -64,6 +65,9 @@ lib.bmqcrc_crc32c_blobs.restype = _int
 lib.bmqcrc_crc32c_blobs.argtypes = [_vp, _u64, _vp, _vp, _u64, _vp, _vp, _vp, _u64,
                                     ctypes.POINTER(Opts)]
 lib.bmqcrc_crc32c_batch_multi.restype = _int
+lib.bmqcrc_crc32c_gather.restype = _int
+lib.bmqcrc_crc32c_gather.argtypes = [ctypes.POINTER(_vp), _vp, _u64, _vp, _vp, _vp, _u64,
+                                     ctypes.POINTER(Opts)]
 lib.bmqcrc_crc32c_batch_multi.argtypes = [_vp, _u64, _vp, _vp, _vp, _vp, _u64, _vp, _int, _u32]
 lib.bmqcrc_reserve.restype = _int
 lib.bmqcrc_reserve.argtypes = [_int, _vp, _u64, _u64, _u32]
@@ -119,11 +123,18 @@ def check_count(n):
     return n
 
 
-def make_opts(device=-1, stream=None, flags=0, seg_bytes=0):
+def make_opts(device=-1, stream=None, flags=0, seg_bytes=0, devices=None):
+    """bmqcrc_opts; `devices` (a sequence of ordinals, repeats allowed) spreads
+    the format-walk entry points over several devices (ABI 2.1)."""
     o = Opts()
     o.struct_size = ctypes.sizeof(Opts)
     o.device = device
     o.stream = stream
     o.flags = flags
     o.seg_bytes = seg_bytes
+    if devices is not None and len(devices) > 1:
+        arr = (ctypes.c_int32 * len(devices))(*devices)
+        o._devices_keep = arr  # the array lives as long as the opts
+        o.ndevices = len(devices)
+        o.devices = ctypes.cast(arr, ctypes.c_void_p)
     return o

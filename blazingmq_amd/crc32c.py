@@ -105,9 +105,9 @@ class Crc32c:
         return verify_batch(arena, offsets, lengths, expected, bad_cap, seg_bytes)
 
     @staticmethod
-    def calculate_blobs(blobs, seeds=None, seg_bytes=0):
-        """Batched Blob overload (bmqcrc_crc32c_blobs) on the GPU."""
-        return calculate_blobs(blobs, seeds, seg_bytes)
+    def calculate_blobs(blobs, seeds=None, seg_bytes=0, gather=True):
+        """Batched Blob overload (bmqcrc_crc32c_gather / bmqcrc_crc32c_blobs) on the GPU."""
+        return calculate_blobs(blobs, seeds, seg_bytes, gather=gather)
 
     @staticmethod
     def calculate_batch(arena, offsets, lengths, seeds=None, out=None, *, seg_bytes=0,
@@ -224,28 +224,49 @@ def verify_batch(arena, offsets, lengths, expected, bad_cap=1 << 20, seg_bytes=0
     return int(nbad.value), idx[:min(int(nbad.value), int(bad_cap))].copy()
 
 
-def calculate_blobs(blobs, seeds=None, seg_bytes=0, device=None):
-    """``bmqp::Crc32c::calculate(blob, seed)`` for a list of Blob on the GPU:
-    buffers are gathered into one staging arena, CRC'd per buffer and chained
-    on the device.  Returns ndarray[uint32]."""
+def calculate_blobs(blobs, seeds=None, seg_bytes=0, device=None, gather=True):
+    """``bmqp::Crc32c::calculate(blob, seed)`` for a list of Blob on the GPU
+    (``Crc32c::calculateBatch(const Blob*)``).  Returns ndarray[uint32].
+
+    gather=True (the C++ overload's path, bmqcrc_crc32c_gather): the blobs'
+    buffers stay where they are and the library copies them once, through a
+    pinned staging ring, into HBM.  gather=False: the buffers are first laid
+    out in one host arena and bmqcrc_crc32c_blobs CRCs each buffer and chains
+    them on the device."""
     bufs, lens, first = [], [], [0]
     for b in blobs:
         nb = b.num_data_buffers()
         for i in range(nb):
             data = b.buffer(i)
             n = len(data) if i < nb - 1 else b.last_data_buffer_length()
-            bufs.append(bytes(data[:n]))
+            bufs.append(data)
             lens.append(n)
         first.append(len(lens))
-    arena = np.frombuffer(b"".join(bufs) + b"\0", dtype=np.uint8)
-    offs = np.zeros(len(lens), dtype=np.uint64)
-    if len(lens) > 1:
-        offs[1:] = np.cumsum(np.asarray(lens[:-1], dtype=np.uint64))
     ln = np.asarray(lens, dtype=np.uint32)
     fb = np.asarray(first, dtype=np.uint64)
     sd = None if seeds is None else np.ascontiguousarray(seeds, dtype=np.uint32)
+    if sd is not None and sd.size != len(blobs):
+        raise ValueError("seeds must have one entry per blob")
     out = np.empty(len(blobs), dtype=np.uint32)
     o = _native.make_opts(device=-1 if device is None else device, seg_bytes=seg_bytes)
+    if gather:
+        keep = [_as_bytes_ptr(bytes(d) if isinstance(d, (bytes, bytearray, memoryview)) else d)
+                for d in bufs]
+        ptrs = (ctypes.c_void_p * max(len(keep), 1))(*[k[0] for k in keep])
+        for k, n in zip(keep, lens):
+            if n > k[1]:
+                raise ValueError("buffer shorter than its data length")
+        _native.check(_native.lib.bmqcrc_crc32c_gather(
+            ptrs, ln.ctypes.data if ln.size else None, ln.size, fb.ctypes.data,
+            sd.ctypes.data if sd is not None else None, out.ctypes.data, len(blobs),
+            ctypes.byref(o)))
+        del keep
+        return out
+    arena = np.frombuffer(b"".join(bytes(d[:n]) for d, n in zip(bufs, lens)) + b"\0",
+                          dtype=np.uint8)
+    offs = np.zeros(len(lens), dtype=np.uint64)
+    if len(lens) > 1:
+        offs[1:] = np.cumsum(np.asarray(lens[:-1], dtype=np.uint64))
     _native.check(_native.lib.bmqcrc_crc32c_blobs(
         arena.ctypes.data, arena.size, offs.ctypes.data if ln.size else None,
         ln.ctypes.data if ln.size else None, ln.size, fb.ctypes.data,

@@ -79,7 +79,7 @@ def append_record(advisory, record_type=UPDATE, elector_term=0, sequence_number=
     return body + value.to_bytes(4, "big")
 
 
-def validate_log(log, expected_log_id=None, device=-1):
+def validate_log(log, expected_log_id=None, device=-1, devices=None):
     """``ClusterStateLedgerUtil::validateLog`` over a whole log buffer.
 
     Returns (rc, offset, bad_record_offset): rc is the reference's result
@@ -91,7 +91,7 @@ def validate_log(log, expected_log_id=None, device=-1):
     if expected_log_id is not None:
         key = ctypes.create_string_buffer(bytes(expected_log_id), 5)
     rc, off, bad = ctypes.c_int(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
-    opts = N.make_opts(device=device)
+    opts = N.make_opts(device=device, devices=devices)
     N.check(N.lib.bmqcrc_csl_validate(
         ctypes.c_void_p(a.ctypes.data) if a.size else None, a.size, key, ctypes.byref(rc),
         ctypes.byref(off), ctypes.byref(bad), ctypes.byref(opts)))

@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -114,10 +115,24 @@ struct Workspace {
     // costs speed (k_fold then maps segments by binary search).
     uint32_t* hint_host = nullptr;
     uint32_t* hint_dev = nullptr;
+    // Pinned staging ring for gathered host buffers (bmqcrc_crc32c_gather):
+    // kGatherSlots chunks of kGatherChunk bytes, each reusable once the event
+    // recorded after its H2D copy has completed.
+    uint8_t* pin = nullptr;
+    hipEvent_t pin_ev[16] = {};
+    bool pin_used[16] = {};
     ~Workspace()
     {
         if (hint_host) {
             (void)hipHostFree(hint_host);
+        }
+        if (pin) {
+            (void)hipHostFree(pin);
+        }
+        for (hipEvent_t e : pin_ev) {
+            if (e) {
+                (void)hipEventDestroy(e);
+            }
         }
         for (auto& v : {timing, spare}) {
             for (auto& e : v) {
@@ -684,6 +699,223 @@ int verify_locked(Ctx& c, Workspace* w, const bmqcrc_opts& o, uint32_t seg, bool
     return 0;
 }
 
+// Library-owned stream k of a device (a device listed twice in
+// bmqcrc_opts.devices gets two streams, hence two workspaces).
+int internal_stream(int dev, int k, hipStream_t* out)
+{
+    static std::map<std::pair<int, int>, hipStream_t> streams;
+    std::lock_guard<std::mutex> g(g_mu);
+    hipStream_t& s = streams[std::make_pair(dev, k)];
+    if (!s) {
+        HIP_TRY(hipSetDevice(dev));
+        HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    }
+    *out = s;
+    return 0;
+}
+
+// bmqcrc_verify_host_overlapped over several devices (bmqcrc_opts.ndevices >
+// 1): the arena is cut into ndevices contiguous byte ranges; one thread per
+// range copies it to its device over that device's PCIe link while the
+// calling thread walks the format, then verifies (or computes) the messages
+// lying wholly inside its range.  The few messages that straddle a cut are
+// gathered into a small arena and done by the first range's thread
+// afterwards.  Results are merged in message order: n_bad is the sum, `bad`
+// the lowest min(n_bad, bad_cap) indices overall.
+int verify_host_multi(const void* arena, uint64_t arena_bytes, bmqcrc_prepare_fn prepare,
+                      void* pctx, uint64_t* n_bad, std::vector<uint64_t>* bad, uint64_t bad_cap,
+                      const bmqcrc_opts& o, uint32_t seg, std::vector<uint32_t>* crcs,
+                      uint64_t* n_written)
+{
+    const uint32_t nd = o.ndevices;
+    if (nd > 64) {
+        return fail(BMQCRC_EINVAL, "at most 64 device listings");
+    }
+    const int have = device_count_raw();
+    std::vector<int> devs(nd);
+    for (uint32_t d = 0; d < nd; ++d) {
+        devs[d] = o.devices ? o.devices[d] : (int)d;
+        if (devs[d] < 0 || (have > 0 && devs[d] >= have)) {
+            return fail(BMQCRC_EINVAL, "device ordinal out of range");
+        }
+    }
+    const uint64_t* off = nullptr;
+    const uint32_t* len = nullptr;
+    const uint32_t* exp = nullptr;
+    uint64_t n = 0;
+    if (have <= 0) {
+        // no usable device: a malformed input is still reported first
+        const int prc = prepare(pctx, &off, &len, &exp, &n);
+        if (prc || n == 0) {
+            return prc;
+        }
+        return fail(BMQCRC_ENODEV, "no HIP device available (batch CRC32C runs only on the GPU)");
+    }
+    std::vector<uint64_t> cut(nd + 1, arena_bytes);
+    cut[0] = 0;
+    for (uint32_t d = 1; d < nd; ++d) {
+        cut[d] = (arena_bytes / nd * d) & ~127ull;
+    }
+    std::vector<int> rcs(nd, 0);
+    std::vector<std::string> errs(nd);
+    std::vector<uint64_t> nb(nd, 0);
+    std::vector<std::vector<uint64_t>> bads(nd);
+    std::vector<uint32_t> owner;  // per message: its range, or nd (straddles a cut)
+    std::mutex mu;
+    std::condition_variable cv;
+    bool walked = false, walk_ok = false;
+    auto slice = [&](uint32_t t) {
+        const int dev = devs[t];
+        hipStream_t st = nullptr;
+        Ctx c;
+        int rc = internal_stream(dev, (int)t, &st);
+        if (!rc) {
+            rc = open_ctx(dev, (void*)st, &c);
+        }
+        std::unique_lock<std::mutex> lk;
+        if (!rc) {
+            lk = std::unique_lock<std::mutex>(c.w->mu);
+            rc = stage(c, c.w->arena, (const uint8_t*)arena + cut[t], cut[t + 1] - cut[t]);
+        }
+        if (!rc && hipStreamSynchronize(c.s) != hipSuccess) {
+            rc = fail(BMQCRC_EIO, "staging the arena range failed");
+        }
+        {
+            std::unique_lock<std::mutex> wl(mu);
+            cv.wait(wl, [&] { return walked; });
+        }
+        if (rc || !walk_ok) {
+            rcs[t] = rc;
+            errs[t] = t_err;
+            return;
+        }
+        // this range's messages (and, for range 0, then the straddlers)
+        for (uint32_t pass = 0; pass < (t == 0 ? 2u : 1u) && !rc; ++pass) {
+            const uint32_t want = pass == 0 ? t : nd;
+            std::vector<uint64_t> gi, lo;
+            std::vector<uint32_t> ll, le;
+            std::vector<uint8_t> packed;
+            for (uint64_t i = 0; i < n; ++i) {
+                if (owner[i] != want) {
+                    continue;
+                }
+                gi.push_back(i);
+                ll.push_back(len[i]);
+                le.push_back(exp ? exp[i] : 0u);
+                if (pass == 0) {
+                    lo.push_back(off[i] - cut[t]);
+                } else {
+                    lo.push_back(packed.size());
+                    packed.insert(packed.end(), (const uint8_t*)arena + off[i],
+                                  (const uint8_t*)arena + off[i] + len[i]);
+                }
+            }
+            if (gi.empty()) {
+                continue;
+            }
+            const uint64_t m = gi.size();
+            const bool staged = pass == 0;
+            const void* abase = staged ? (const void*)((const uint8_t*)arena + cut[t])
+                                       : (const void*)packed.data();
+            const uint64_t abytes = staged ? cut[t + 1] - cut[t] : packed.size();
+            if (crcs) {
+                std::vector<uint32_t> part(m);
+                if ((!staged && (rc = stage(c, c.w->arena, abase, abytes))) ||
+                    (rc = stage(c, c.w->offsets, lo.data(), 8 * m)) ||
+                    (rc = stage(c, c.w->lengths, ll.data(), 4 * m)) ||
+                    (rc = c.w->out.ensure(4 * m)) ||
+                    (rc = run_batch(c, o.flags, seg, c.w->arena.p, abytes,
+                                    (const uint64_t*)c.w->offsets.p,
+                                    (const uint32_t*)c.w->lengths.p, nullptr,
+                                    (uint32_t*)c.w->out.p, m, max_length(ll.data(), m)))) {
+                    break;
+                }
+                if (hipMemcpyAsync(part.data(), c.w->out.p, 4 * m, hipMemcpyDeviceToHost, c.s) !=
+                        hipSuccess ||
+                    hipStreamSynchronize(c.s) != hipSuccess) {
+                    rc = fail(BMQCRC_EIO, "copying the CRCs back failed");
+                    break;
+                }
+                for (uint64_t k = 0; k < m; ++k) {
+                    (*crcs)[gi[k]] = part[k];
+                }
+                continue;
+            }
+            uint64_t nbad = 0, nw = 0;
+            std::vector<uint64_t> lb(std::min<uint64_t>(bad_cap, m));
+            if ((rc = verify_locked(c, c.w, o, seg, staged, abase, abytes, lo.data(), ll.data(),
+                                    le.data(), m, &nbad, lb.data(), lb.size(), &nw))) {
+                break;
+            }
+            nb[t] += nbad;
+            for (uint64_t k = 0; k < nw; ++k) {
+                bads[t].push_back(gi[lb[k]]);
+            }
+        }
+        rcs[t] = rc;
+        errs[t] = t_err;
+    };
+    std::vector<std::thread> th;
+    for (uint32_t t = 0; t < nd; ++t) {
+        th.emplace_back(slice, t);
+    }
+    const int prc = prepare(pctx, &off, &len, &exp, &n);
+    int rc = prc;
+    if (!rc && n > 0xFFFFFFFFull) {
+        rc = fail(BMQCRC_EINVAL, "at most 2^32-1 messages per batch");
+    }
+    if (!rc) {
+        rc = check_ranges(off, len, n, arena_bytes);
+    }
+    if (!rc) {
+        owner.resize(n);
+        for (uint64_t i = 0; i < n; ++i) {
+            uint32_t t = (uint32_t)(std::upper_bound(cut.begin(), cut.end(), off[i]) - cut.begin());
+            t = std::min(t == 0 ? 0u : t - 1u, nd - 1);
+            owner[i] = off[i] + len[i] <= cut[t + 1] ? t : nd;
+        }
+        if (crcs) {
+            crcs->assign(n, 0);
+        }
+    }
+    const std::string walk_err = t_err;
+    {
+        std::lock_guard<std::mutex> wl(mu);
+        walked = true;
+        walk_ok = rc == 0;
+    }
+    cv.notify_all();
+    for (auto& t : th) {
+        t.join();
+    }
+    if (rc) {  // the walk's error (malformed input) takes precedence
+        t_err = walk_err;
+        return rc;
+    }
+    for (uint32_t t = 0; t < nd; ++t) {
+        if (rcs[t]) {
+            return fail(rcs[t], "device " + std::to_string(devs[t]) + ": " + errs[t]);
+        }
+    }
+    if (crcs) {
+        return 0;
+    }
+    uint64_t total_bad = 0;
+    std::vector<uint64_t> all;
+    for (uint32_t t = 0; t < nd; ++t) {
+        total_bad += nb[t];
+        all.insert(all.end(), bads[t].begin(), bads[t].end());
+    }
+    std::sort(all.begin(), all.end());
+    const uint64_t take = std::min<uint64_t>(all.size(), bad_cap);
+    bad->assign(std::min(bad_cap, n), 0);
+    std::copy(all.begin(), all.begin() + take, bad->begin());
+    *n_bad = total_bad;
+    if (n_written) {
+        *n_written = take;
+    }
+    return 0;
+}
 
 }  // namespace
 
@@ -717,6 +949,10 @@ int bmqcrc_verify_host_overlapped(const void* arena, uint64_t arena_bytes,
     }
     if (o.flags & (BMQCRC_F_DEVICE_PTRS | BMQCRC_F_ASYNC)) {
         return fail(BMQCRC_EINVAL, "overlapped verify takes host buffers, synchronously");
+    }
+    if (o.ndevices > 1) {
+        return verify_host_multi(arena, arena_bytes, prepare, pctx, n_bad, bad, bad_cap, o, seg,
+                                 crcs, n_written);
     }
     Ctx c;
     if (rc || (rc = open_ctx(dev, o.stream, &c))) {
@@ -862,6 +1098,162 @@ int bmqcrc_crc32c_blobs(const void* arena, uint64_t arena_bytes, const uint64_t*
     } else if (!(o.flags & BMQCRC_F_ASYNC)) {
         HIP_TRY(hipStreamSynchronize(c.s));
     }
+    return 0;
+}
+
+// Scattered host buffers (a bdlbb::Blob's data buffers) -> one contiguous
+// device arena, through the workspace's pinned ring: kGatherThreads host
+// threads each copy their chunks into pinned slots and enqueue the slot's H2D
+// copy at once, so gathering chunk k+1 overlaps the PCIe transfer of chunk k
+// (no pageable staging copy, no second host copy).  Message m is then the
+// contiguous range of its buffers and the whole batch is one fold launch.
+constexpr uint64_t kGatherChunk = 4ull << 20;
+constexpr int kGatherSlots = 16;
+constexpr int kGatherThreads = 8;
+
+int bmqcrc_crc32c_gather(const void* const* bufs, const uint32_t* buf_lengths, uint64_t nbuf,
+                         const uint64_t* msg_first_buf, const uint32_t* seeds, uint32_t* out,
+                         uint64_t n, const bmqcrc_opts* opts)
+{
+    t_err.clear();
+    DeviceGuard keep_device;
+    if (n == 0) {
+        return 0;
+    }
+    if (!msg_first_buf || !out || (nbuf && (!bufs || !buf_lengths))) {
+        return fail(BMQCRC_EINVAL, "null pointer argument");
+    }
+    if (nbuf > 0xFFFFFFFFull || n > 0xFFFFFFFFull) {
+        return fail(BMQCRC_EINVAL, "at most 2^32-1 buffers and messages per call");
+    }
+    for (uint64_t m = 0; m < n; ++m) {
+        if (msg_first_buf[m] > msg_first_buf[m + 1] || msg_first_buf[m + 1] > nbuf) {
+            return fail(BMQCRC_EINVAL, "msg_first_buf must be non-decreasing and <= nbuf");
+        }
+    }
+    // Arena layout: buffers [b0, b1) back to back, in order.
+    const uint64_t b0 = msg_first_buf[0], b1 = msg_first_buf[n];
+    std::vector<uint64_t> boff(b1 - b0 + 1, 0);
+    for (uint64_t b = b0; b < b1; ++b) {
+        if (buf_lengths[b] && !bufs[b]) {
+            return fail(BMQCRC_EINVAL, "buffer " + std::to_string(b) + " is NULL with a length");
+        }
+        boff[b - b0 + 1] = boff[b - b0] + buf_lengths[b];
+    }
+    const uint64_t total = boff.back();
+    std::vector<uint64_t> moff(n);
+    std::vector<uint32_t> mlen(n);
+    uint64_t maxlen = 0;
+    for (uint64_t m = 0; m < n; ++m) {
+        moff[m] = boff[msg_first_buf[m] - b0];
+        const uint64_t len = boff[msg_first_buf[m + 1] - b0] - moff[m];
+        if (len > 0xFFFFFFFFull) {
+            return fail(BMQCRC_EINVAL, "message " + std::to_string(m) + " is longer than 2^32-1");
+        }
+        mlen[m] = (uint32_t)len;
+        maxlen = std::max(maxlen, len);
+    }
+    // argument errors above are reported before a missing device
+    bmqcrc_opts o;
+    uint32_t seg;
+    int dev, rc;
+    if ((rc = parse_opts(opts, &o, &seg, &dev))) {
+        return rc;
+    }
+    if (o.flags & (BMQCRC_F_DEVICE_PTRS | BMQCRC_F_ASYNC)) {
+        return fail(BMQCRC_EINVAL, "gather takes host buffers, synchronously");
+    }
+    Ctx c;
+    if ((rc = open_ctx(dev, o.stream, &c))) {
+        return rc;
+    }
+    Workspace* w = c.w;
+    std::lock_guard<std::mutex> g(w->mu);
+    if ((rc = w->arena.ensure(total + 16))) {
+        return rc;
+    }
+    if (total && !w->pin) {
+        void* h = nullptr;
+        HIP_TRY(hipHostMalloc(&h, kGatherSlots * kGatherChunk, hipHostMallocPortable));
+        w->pin = (uint8_t*)h;
+        for (int sl = 0; sl < kGatherSlots; ++sl) {
+            HIP_TRY(hipEventCreateWithFlags(&w->pin_ev[sl], hipEventDisableTiming));
+        }
+    }
+    const uint64_t nchunks = (total + kGatherChunk - 1) / kGatherChunk;
+    const int nthreads = (int)std::min<uint64_t>(kGatherThreads, nchunks);
+    std::vector<int> trc(std::max(nthreads, 1), 0);
+    std::vector<std::string> terr(trc.size());
+    auto worker = [&](int t) {
+        if (hipSetDevice(dev) != hipSuccess) {
+            trc[t] = BMQCRC_EIO;
+            terr[t] = "hipSetDevice failed in a gather thread";
+            return;
+        }
+        const int per = kGatherSlots / nthreads;  // slots t, t + nthreads, ... are thread t's
+        for (uint64_t ch = (uint64_t)t; ch < nchunks; ch += (uint64_t)nthreads) {
+            const int sl = t + nthreads * (int)((ch / (uint64_t)nthreads) % (uint64_t)per);
+            hipError_t e = hipSuccess;
+            if (w->pin_used[sl]) {
+                e = hipEventSynchronize(w->pin_ev[sl]);  // the slot's previous copy is done
+            }
+            const uint64_t lo = ch * kGatherChunk, hi = std::min(total, lo + kGatherChunk);
+            uint8_t* dst = w->pin + (uint64_t)sl * kGatherChunk;
+            size_t k = (size_t)(std::upper_bound(boff.begin(), boff.end(), lo) - boff.begin()) - 1;
+            for (uint64_t pos = lo; e == hipSuccess && pos < hi;) {
+                if (boff[k + 1] <= pos) {
+                    ++k;  // empty buffers and buffers that end at pos
+                    continue;
+                }
+                const uint64_t take = std::min(hi, boff[k + 1]) - pos;
+                memcpy(dst + (pos - lo), (const uint8_t*)bufs[b0 + k] + (pos - boff[k]), take);
+                pos += take;
+            }
+            if (e == hipSuccess) {
+                e = hipMemcpyAsync((uint8_t*)w->arena.p + lo, dst, hi - lo, hipMemcpyHostToDevice,
+                                   c.s);
+            }
+            if (e == hipSuccess) {
+                e = hipEventRecord(w->pin_ev[sl], c.s);
+            }
+            if (e != hipSuccess) {
+                trc[t] = e == hipErrorOutOfMemory ? BMQCRC_ENOMEM : BMQCRC_EIO;
+                terr[t] = std::string("gather staging: ") + hipGetErrorString(e);
+                return;
+            }
+            w->pin_used[sl] = true;
+        }
+    };
+    if (nthreads == 1) {
+        worker(0);
+    } else if (nthreads > 1) {
+        std::vector<std::thread> th;
+        for (int t = 0; t < nthreads; ++t) {
+            th.emplace_back(worker, t);
+        }
+        for (auto& t : th) {
+            t.join();
+        }
+    }
+    for (size_t t = 0; t < trc.size(); ++t) {
+        if (trc[t]) {
+            (void)hipStreamSynchronize(c.s);  // no copy may still read a slot we hand back
+            return fail(trc[t], terr[t]);
+        }
+    }
+    if ((rc = stage(c, w->offsets, moff.data(), 8 * n)) ||
+        (rc = stage(c, w->lengths, mlen.data(), 4 * n)) ||
+        (seeds && (rc = stage(c, w->seeds, seeds, 4 * n))) || (rc = w->out.ensure(4 * n))) {
+        return rc;
+    }
+    if ((rc = run_batch(c, o.flags, seg, w->arena.p, total, (const uint64_t*)w->offsets.p,
+                        (const uint32_t*)w->lengths.p,
+                        seeds ? (const uint32_t*)w->seeds.p : nullptr, (uint32_t*)w->out.p, n,
+                        maxlen))) {
+        return rc;
+    }
+    HIP_TRY(hipMemcpyAsync(out, w->out.p, 4 * n, hipMemcpyDeviceToHost, c.s));
+    HIP_TRY(hipStreamSynchronize(c.s));
     return 0;
 }
 
@@ -1080,7 +1472,7 @@ const char* bmqcrc_last_error(void)
 
 uint32_t bmqcrc_version(void)
 {
-    return (2u << 16) | 0u;
+    return (2u << 16) | 1u;
 }
 
 }  // extern "C"

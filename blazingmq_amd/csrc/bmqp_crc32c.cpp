@@ -3,8 +3,6 @@
 #include "bmqp_crc32c.h"
 
 #include <stdint.h>
-#include <string.h>
-
 #include <vector>
 
 namespace BloombergLP {
@@ -81,32 +79,23 @@ int Crc32c::calculateBatch(const bdlbb::Blob* blobs,
                            const bmqcrc_opts* opts)
 {
     // Same buffer selection as calculate(const Blob&): every buffer but the
-    // last in full, the last up to lastDataBufferLength().
-    std::vector<uint64_t> off, first(1, 0);
+    // last in full, the last up to lastDataBufferLength().  The buffers stay
+    // where they are; bmqcrc_crc32c_gather copies them once, through a pinned
+    // staging ring, straight to the device.
+    std::vector<const void*> ptr;
     std::vector<uint32_t> len;
-    uint64_t total = 0;
+    std::vector<uint64_t> first(1, 0);
     for (unsigned int b = 0; b < count; ++b) {
         const int nb = blobs[b].numDataBuffers();
         for (int i = 0; i < nb; ++i) {
             const int n = (i + 1 < nb) ? blobs[b].buffer(i).size() : blobs[b].lastDataBufferLength();
-            off.push_back(total);
+            ptr.push_back(blobs[b].buffer(i).data());
             len.push_back(static_cast<uint32_t>(n));
-            total += static_cast<uint64_t>(n);
         }
-        first.push_back(off.size());
+        first.push_back(ptr.size());
     }
-    std::vector<char> arena(total + 1);
-    size_t k = 0;
-    for (unsigned int b = 0; b < count; ++b) {
-        const int nb = blobs[b].numDataBuffers();
-        for (int i = 0; i < nb; ++i, ++k) {
-            if (len[k]) {
-                memcpy(&arena[off[k]], blobs[b].buffer(i).data(), len[k]);
-            }
-        }
-    }
-    const int rc = bmqcrc_crc32c_blobs(arena.data(), total, off.data(), len.data(), len.size(),
-                                       first.data(), seeds, crcs, count, opts);
+    const int rc = bmqcrc_crc32c_gather(ptr.data(), len.data(), len.size(), first.data(), seeds,
+                                        crcs, count, opts);
     if (!gpuFailure(rc)) {
         return rc;
     }

@@ -48,8 +48,9 @@ class PutEventBuilder:
     reference), with ``defer_crc=True`` ``finalize()`` computes all CRCs in one
     batch on the GPU."""
 
-    def __init__(self, defer_crc=True):
+    def __init__(self, defer_crc=True, devices=None):
         self.defer_crc = defer_crc
+        self.devices = devices  # several ordinals: spread the deferred fill over them
         self._chunks = [bytes(EVENT_HEADER_SIZE)]
         self._size = EVENT_HEADER_SIZE
         self._app_off = []   # offset of app data inside the event
@@ -93,7 +94,7 @@ class PutEventBuilder:
         ev[4] = (PROTOCOL_VERSION << 6) | EVENT_TYPE_PUT
         ev[5] = EVENT_HEADER_SIZE // WORD
         if self.defer_crc and self._app_off:
-            opts = N.make_opts()
+            opts = N.make_opts(devices=self.devices)
             n = N.check_count(N.lib.bmqcrc_put_event_fill_crcs(
                 ctypes.c_void_p(ev.ctypes.data), ev.size, ctypes.byref(opts)))
             if n != len(self._app_off):
@@ -127,13 +128,14 @@ class PutMessageIterator:
                 ctypes.c_void_p(pos.ctypes.data), n))
         return off, ln, pos
 
-    def verify_crcs(self, bad_cap=1 << 16, device=-1):
+    def verify_crcs(self, bad_cap=1 << 16, device=-1, devices=None):
         """Check every PutHeader CRC against its application data in one GPU
-        batch.  Returns (n_messages, n_bad, bad message indices)."""
+        batch (``devices``: spread over several devices, bmqcrc_opts.ndevices).
+        Returns (n_messages, n_bad, bad message indices)."""
         ev = np.ascontiguousarray(self.ev)
         n_msgs, n_bad = ctypes.c_uint64(0), ctypes.c_uint64(0)
         bad = np.zeros(max(int(bad_cap), 1), np.uint64)
-        opts = N.make_opts(device=device)
+        opts = N.make_opts(device=device, devices=devices)
         N.check(N.lib.bmqcrc_put_event_verify(
             ctypes.c_void_p(ev.ctypes.data), ev.size, ctypes.byref(n_msgs), ctypes.byref(n_bad),
             ctypes.c_void_p(bad.ctypes.data), int(bad_cap), ctypes.byref(opts)))

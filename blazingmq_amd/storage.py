@@ -335,7 +335,8 @@ def scan_partition(journal, data, with_csl=False, queue_keys=()):
     return out
 
 
-def verify_partition(journal, data, bad_cap=1 << 20, device=-1, with_csl=False, queue_keys=()):
+def verify_partition(journal, data, bad_cap=1 << 20, device=-1, with_csl=False, queue_keys=(),
+                     devices=None):
     """Recovery CRC check of a whole partition: one native walk selecting the
     records FileStore::recoverMessages CRCs, one batched GPU verify
     (``bmqcrc_recover_verify``).
@@ -344,13 +345,15 @@ def verify_partition(journal, data, bad_cap=1 << 20, device=-1, with_csl=False, 
     error_record_offset).  A mismatch is what the reference reports with
     BMQTSK_ALARMLOG_ALARM("RECOVERY") (mqbs_filestore.cpp:2613-2624) and
     keeps going; offsets come in the order it raises them (backward).
+    ``devices`` (several ordinals, repeats allowed) spreads the DATA file's
+    staging and verify over those devices (bmqcrc_opts.ndevices).
     """
     j, d = np.ascontiguousarray(_as_u8(journal)), np.ascontiguousarray(_as_u8(data))
     cfg, _keys = _cfg(with_csl, queue_keys)
     n_msgs, n_bad = ctypes.c_uint64(0), ctypes.c_uint64(0)
     rrc, err = ctypes.c_int(0), ctypes.c_uint64(0)
     bad = np.zeros(max(int(bad_cap), 1), np.uint64)
-    opts = N.make_opts(device=device)
+    opts = N.make_opts(device=device, devices=devices)
 
     def run():
         return N.check(N.lib.bmqcrc_recover_verify(

@@ -63,6 +63,19 @@ typedef struct bmqcrc_opts {
     uint32_t flags;       /* BMQCRC_F_* */
     uint32_t seg_bytes;   /* segment size in bytes, multiple of 128 in [256, 2^30]; 0 = automatic
                              from the batch's size (256 B - 64 KiB) */
+    /* ABI 2.1.  Format-walk entry points (bmqcrc_protocol.h: recovery verify,
+     * PUT-event fill/verify, ledger validate) only: with ndevices > 1 the
+     * input buffer is cut into ndevices contiguous byte ranges, each copied to
+     * its own device (its own PCIe link) while the calling thread walks the
+     * format; each device then verifies the messages lying in its range, and
+     * the few that straddle a cut are done by the first device.  Results are
+     * identical to the single-device call.  devices == NULL means
+     * 0..ndevices-1; a device may be listed more than once (each listing gets
+     * a library-owned stream); `device` and `stream` are then ignored.
+     * ndevices 0 or 1: the single device above.  Callers built against ABI
+     * 2.0 (smaller struct_size) get 0. */
+    uint32_t ndevices;
+    const int32_t* devices;
 } bmqcrc_opts;
 
 /* ---- scalar (host CPU) -------------------------------------------------- */
@@ -111,6 +124,20 @@ int bmqcrc_crc32c_blobs(const void* arena, uint64_t arena_bytes, const uint64_t*
                         const uint32_t* buf_lengths, uint64_t nbuf,
                         const uint64_t* msg_first_buf, const uint32_t* seeds, uint32_t* out,
                         uint64_t n, const bmqcrc_opts* opts);
+
+/* The same Blob CRCs when the buffers are scattered in host memory (a
+ * bdlbb::Blob's data buffers, as Crc32c::calculateBatch(const Blob*) passes
+ * them): message m is the concatenation of bufs[msg_first_buf[m] ..
+ * msg_first_buf[m+1]) with their buf_lengths, out[m] = its CRC chained from
+ * seeds ? seeds[m] : 0.  Host pointers only (BMQCRC_F_DEVICE_PTRS and
+ * BMQCRC_F_ASYNC are EINVAL), synchronous.  The buffers are gathered by
+ * several host threads through a pinned staging ring whose chunks go to HBM
+ * while the next ones are gathered (one host copy, no pageable staging), then
+ * CRC'd as one batch on the device.  A message may be at most 2^32-1 bytes.
+ * GPU only. */
+int bmqcrc_crc32c_gather(const void* const* bufs, const uint32_t* buf_lengths, uint64_t nbuf,
+                         const uint64_t* msg_first_buf, const uint32_t* seeds, uint32_t* out,
+                         uint64_t n, const bmqcrc_opts* opts);
 
 /* Host-pointer batch sharded over `ndev` devices: messages are split into
  * contiguous byte-balanced slices, one per device, each on its own stream,

@@ -52,10 +52,11 @@ struct Crc32c {
                               const bmqcrc_opts* opts = 0);
 
     /// Batched Blob overload: `crcs[i] = calculate(blobs[i], seeds ? seeds[i] :
-    /// 0)` for `i < count`, computed on an MI355X (the blobs' buffers are
-    /// gathered into one staging arena, CRC'd per buffer and chained on the
-    /// device).  Returns 0 or a negative BMQCRC_E* code; without a usable GPU
-    /// it finishes on the host like the overload above.
+    /// 0)` for `i < count`, computed on an MI355X (bmqcrc_crc32c_gather: the
+    /// blobs' buffers are copied once, through a pinned staging ring, into
+    /// HBM, and every blob is folded as one message).  Returns 0 or a
+    /// negative BMQCRC_E* code; without a usable GPU it finishes on the host
+    /// like the overload above.
     static int calculateBatch(const bdlbb::Blob* blobs,
                               unsigned int       count,
                               const unsigned int* seeds,

@@ -130,6 +130,25 @@ def test_batch_rejects_unknown_flags():
         assert rc == N.BMQCRC_ENODEV
 
 
+def test_gather_refuses_without_gpu():
+    """bmqcrc_crc32c_gather is a GPU-only batch entry point: ENODEV here, and
+    argument errors are still reported first."""
+    import ctypes
+    from blazingmq_amd import _native as N
+    bufs = [np.frombuffer(b"hello ", np.uint8), np.frombuffer(b"world", np.uint8)]
+    ptrs = (ctypes.c_void_p * 2)(*[b.ctypes.data for b in bufs])
+    lens = np.array([6, 5], np.uint32)
+    first = np.array([0, 2], np.uint64)
+    out = np.zeros(1, np.uint32)
+    o = N.make_opts()
+    assert N.lib.bmqcrc_crc32c_gather(ptrs, lens.ctypes.data, 2, first.ctypes.data, None,
+                                      out.ctypes.data, 1, ctypes.byref(o)) == N.BMQCRC_ENODEV
+    bad_first = np.array([1, 0], np.uint64)
+    assert N.lib.bmqcrc_crc32c_gather(ptrs, lens.ctypes.data, 2, bad_first.ctypes.data, None,
+                                      out.ctypes.data, 1, ctypes.byref(o)) == N.BMQCRC_EINVAL
+    # the C++ Blob overload finishes on the host instead (checked in the self-test)
+
+
 def test_host_register_refuses_without_gpu():
     import ctypes
     import numpy as np

@@ -149,9 +149,11 @@ def test_csl_validate_large_log_first_bad(cuda):
     assert csl.validate_log(bytes(b)) == (csl.INVALID_CHECKSUM, 0, int(ends[1234]))
 
 
-def test_blobs_batch(cuda, golden):
+@pytest.mark.parametrize("gather", [True, False])
+def test_blobs_batch(cuda, golden, gather):
     blobs = [Blob(bytes.fromhex(h) for h in v["buffers_hex"]) for v in golden["blob"]]
-    assert Crc32c.calculate_blobs(blobs).tolist() == [v["crc"] for v in golden["blob"]]
+    assert Crc32c.calculate_blobs(blobs, gather=gather).tolist() == \
+        [v["crc"] for v in golden["blob"]]
     rng = np.random.default_rng(10)
     blobs, seeds, exp = [], [], []
     for _ in range(400):
@@ -162,5 +164,97 @@ def test_blobs_batch(cuda, golden):
         blobs.append(Blob(parts))
         seeds.append(seed)
         exp.append(oracle.blob(parts, seed))
-    got = Crc32c.calculate_blobs(blobs, seeds=np.array(seeds, np.uint32))
+    got = Crc32c.calculate_blobs(blobs, seeds=np.array(seeds, np.uint32), gather=gather)
     assert got.tolist() == exp
+    # a shorter last data buffer (lastDataBufferLength, bmqp_crc32c.cpp:62-64)
+    b = Blob([b"abcdefgh", b"ijklmnop"])
+    b.set_last_data_buffer_length(3)
+    assert Crc32c.calculate_blobs([b], gather=gather).tolist() == [oracle.crc32c(b"abcdefghijk")]
+
+
+def test_gather_spans_many_staging_chunks(cuda):
+    """bmqcrc_crc32c_gather over ~80 MiB of separately allocated buffers: more
+    chunks than the pinned ring has slots (every slot reused, several gather
+    threads), buffers and messages crossing chunk boundaries, empty buffers and
+    empty messages, seeds; then the same call again on the warm workspace."""
+    from blazingmq_amd import _native as N
+    import ctypes
+    rng = np.random.default_rng(31)
+    sizes = rng.choice([0, 1, 7, 4096, 65536, 1 << 20, 3_000_001], size=90,
+                       p=[.1, .1, .1, .3, .2, .15, .05])
+    bufs = [rng.integers(0, 256, size=int(k), dtype=np.uint8) for k in sizes]
+    cuts = np.sort(rng.choice(np.arange(1, len(bufs)), size=14, replace=False))
+    first = np.concatenate([[0], cuts, [len(bufs)], [len(bufs)]]).astype(np.uint64)  # + empty msg
+    n = first.size - 1
+    seeds = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    ptrs = (ctypes.c_void_p * len(bufs))(*[b.ctypes.data for b in bufs])
+    lens = np.array([b.size for b in bufs], np.uint32)
+    exp = [oracle.blob([bufs[k].tobytes() for k in range(int(first[m]), int(first[m + 1]))],
+                       int(seeds[m])) for m in range(n)]
+    for _ in range(2):
+        out = np.zeros(n, np.uint32)
+        o = N.make_opts()
+        N.check(N.lib.bmqcrc_crc32c_gather(ptrs, lens.ctypes.data, len(bufs), first.ctypes.data,
+                                           seeds.ctypes.data, out.ctypes.data, n, ctypes.byref(o)))
+        assert out.tolist() == exp
+    # host pointers only
+    o = N.make_opts(flags=N.BMQCRC_F_DEVICE_PTRS)
+    assert N.lib.bmqcrc_crc32c_gather(ptrs, lens.ctypes.data, len(bufs), first.ctypes.data, None,
+                                      out.ctypes.data, n, ctypes.byref(o)) == N.BMQCRC_EINVAL
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+def test_walks_spread_over_devices(cuda, devices):
+    """bmqcrc_opts.ndevices (ABI 2.1): the format-walk entry points cut the
+    input buffer into byte ranges, stage and verify each on its own device
+    listing (here the one GPU listed several times: each listing is its own
+    stream and workspace), messages straddling a cut on the first listing.
+    Results equal the single-device call exactly: counts, alarm offsets and
+    their order, bounded reports, filled CRCs, the ledger's first bad record."""
+    rng = np.random.default_rng(40)
+    sizes = rng.integers(0, 30000, size=6000)
+    apps = [rng.integers(0, 256, size=int(k), dtype=np.uint8).tobytes() for k in sizes]
+    j, d = storage.write_partition(apps)
+    scan = storage.scan_partition(j, d)
+    live = [i for i in range(len(apps)) if scan["app_length"][i] > 0]
+    victims = sorted(int(v) for v in rng.choice(live, size=41, replace=False))
+    for i in victims:
+        d[int(scan["app_offset"][i]) + int(scan["app_length"][i]) - 1] ^= 0x04
+    one = storage.verify_partition(j, d)
+    many = storage.verify_partition(j, d, devices=devices)
+    assert one["n_bad"] == many["n_bad"] == len(victims)
+    assert many["bad_record_offsets"].tolist() == one["bad_record_offsets"].tolist() == \
+        scan["record_offset"][victims].tolist()
+    assert storage.verify_partition(j, d, bad_cap=7, devices=devices)[
+        "bad_record_offsets"].tolist() == one["bad_record_offsets"][:7].tolist()
+    from test_recovery_selection import rich_partition
+    rj, rd, expected, _ = rich_partition(seed=2)
+    r1, rm = storage.verify_partition(rj, rd), storage.verify_partition(rj, rd, devices=devices)
+    assert (rm["n_messages"], rm["n_bad"], rm["recovery_rc"]) == \
+        (r1["n_messages"], r1["n_bad"], r1["recovery_rc"]) == (len(expected), 0, 0)
+    # PUT events: deferred fill over several listings == immediate CRCs
+    papps = [rng.integers(0, 256, size=int(k), dtype=np.uint8).tobytes()
+             for k in rng.integers(0, 9000, size=700)]
+    evs = []
+    for defer, devs in ((False, None), (True, devices)):
+        b = PutEventBuilder(defer_crc=defer, devices=devs)
+        for i, a in enumerate(papps):
+            b.pack_message(a, queue_id=i, guid=i.to_bytes(16, "big"))
+        evs.append(b.finalize())
+    assert np.array_equal(evs[0], evs[1])
+    off, ln, _ = PutMessageIterator(evs[1]).scan()
+    ev = evs[1].copy()
+    pv = [i for i in (5, 300, 699) if ln[i] > 0]
+    for i in pv:
+        ev[int(off[i])] ^= 0x01
+    n, n_bad, bad = PutMessageIterator(ev).verify_crcs(devices=devices)
+    assert (n, n_bad, bad.tolist()) == (len(papps), len(pv), pv)
+    # ledger: the first corrupt record, as with one device
+    log, recs = _csl_log(3000, rng)
+    ends = np.cumsum([csl.FILE_HEADER_SIZE] + [len(r) for r in recs])
+    b = bytearray(log)
+    for k in (2900, 1500, 2000):
+        b[int(ends[k]) + csl.RECORD_HEADER_SIZE] ^= 0x01
+    assert csl.validate_log(bytes(b), devices=devices) == csl.validate_log(bytes(b)) == \
+        (csl.INVALID_CHECKSUM, 0, int(ends[1500]))
+    assert csl.validate_log(log, devices=devices)[:2] == (csl.SUCCESS, len(log))

@@ -216,3 +216,31 @@ def test_gpu_only_walks_refuse_without_device():
     with pytest.raises(N.BmqCrcError) as e:
         csl.validate_log(log, KEY)
     assert e.value.rc == N.BMQCRC_ENODEV
+
+
+@pytest.mark.skipif(not NO_GPU, reason="checks the no-device refusal")
+def test_multi_device_walks_refuse_without_device():
+    """bmqcrc_opts.ndevices > 1 keeps the single-device contract: a malformed
+    input is reported before a missing device, an empty selection needs no
+    device, otherwise ENODEV (never a CPU result)."""
+    j, d = _fixture()
+    with pytest.raises(N.BmqCrcError) as e:
+        storage.verify_partition(j, d, devices=[0, 0])
+    assert e.value.rc == N.BMQCRC_ENODEV
+    w = storage.PartitionWriter()
+    assert storage.verify_partition(*w.files(), devices=[0, 1])["n_messages"] == 0
+    bad = bytearray(_event([b"abc"]).tobytes() if hasattr(_event([b"abc"]), "tobytes")
+                    else _event([b"abc"]))
+    bad[8] ^= 0xFF  # PutHeader words: malformed
+    with pytest.raises((N.BmqCrcError, ValueError)) as e:
+        PutMessageIterator(bytes(bad)).verify_crcs(devices=[0, 0])
+    if isinstance(e.value, N.BmqCrcError):
+        assert e.value.rc == N.BMQCRC_EINVAL
+    log, _ = _log(2)
+    with pytest.raises(N.BmqCrcError) as e:
+        csl.validate_log(log, KEY, devices=[0, 0, 0])
+    assert e.value.rc == N.BMQCRC_ENODEV
+    # more listings than the ABI allows
+    with pytest.raises(N.BmqCrcError) as e:
+        csl.validate_log(log, KEY, devices=list(range(65)))
+    assert e.value.rc == N.BMQCRC_EINVAL
