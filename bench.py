@@ -171,6 +171,11 @@ def cpu_baseline(lens_np, seed, seconds):
         "cores": threads,
         "kind": "port",
         "single_thread_value": round(gib / t1, 3),
+        "host_threads": os.cpu_count(),
+        "not_measured": "nproc/8 (%d threads, one GPU's share of an 8-GPU node) and all %d "
+                        "threads: a one-GPU job on this pool may use %d threads "
+                        "(OMP_NUM_THREADS); the rest of the shared host is not ours to load"
+                        % ((os.cpu_count() or 8) // 8, os.cpu_count() or 0, threads),
         "sample": "first %d msgs (%.0f MiB) of the same synthetic batch, %d passes on %d "
                   "threads (this GPU's share of the host: OMP_NUM_THREADS, 16 per GPU on the "
                   "pool; the whole host is not ours to load); SSE4.2 crc32q 3-way interleaved "

@@ -58,3 +58,17 @@ def test_gpus_must_match_world_size():
                         "--launch-check"], capture_output=True, text=True, timeout=120,
                        cwd=ROOT, env=env)
     assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
+
+
+def test_cpu_baseline_states_its_thread_counts():
+    """The bench line's cpu_baseline: measured on this GPU's thread share and
+    on one thread, with the host's thread count and the counts it did not
+    measure stated."""
+    sys.path.insert(0, ROOT)
+    import numpy as np
+
+    import bench
+    cb = bench.cpu_baseline(np.full(2048, 4096, np.uint32), 2, 0.05)
+    assert cb["kind"] == "port" and cb["value"] > 0 and cb["single_thread_value"] > 0
+    assert cb["cores"] == bench.host_threads() and cb["host_threads"] == os.cpu_count()
+    assert "nproc/8" in cb["not_measured"]
