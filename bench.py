@@ -631,6 +631,9 @@ def main():
             res["rehearsal_single_gpu"] = True
             res["ranks_on_one_gpu"] = world
         if strong is not None:
+            if rehearsal:  # N ranks on one GPU: not a scaling point
+                strong["n_gpus"] = 1
+                strong["ranks_on_one_gpu"] = world
             res["strong_scaling"] = strong
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(lens_np, seed, args.cpu_seconds)

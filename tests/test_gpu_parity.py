@@ -5,6 +5,8 @@ and the reference's golden vectors; BASELINE-size cases compare sampled
 messages plus size-independent properties.  Mirrors the reference's own test
 plan (bmqp_crc32c.t.cpp test1-test8, fuzz s_bmqfuzz_bmqp_crc32c.fuzz.cpp).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -479,3 +481,24 @@ def test_speculative_single_launch(cuda):
                           rng.integers(0, 4, size=n) == 0, 0, short())),
                       ("spec", short())):
         run(lens, tag)
+
+
+def test_ranks_shard_a_batch_on_the_gpu(cuda):
+    """N ranks, one process each (torch.distributed.run, gloo for the result
+    hand-off only), each CRCs its byte-balanced slice of one Zipf batch
+    through the HIP path on device rank % device_count, every CRC checked
+    against the oracle; rank 0 checks the stitched batch.  On a one-GPU box
+    both ranks share the GPU; on a node they run on distinct devices."""
+    import socket
+    import subprocess
+    import sys
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    worker = os.path.join(os.path.dirname(__file__), "mp_shard_worker.py")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+                        "--master-port", str(port), worker],
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "bit_exact=True" in r.stdout
