@@ -258,3 +258,31 @@ def test_walks_spread_over_devices(cuda, devices):
     assert csl.validate_log(bytes(b), devices=devices) == csl.validate_log(bytes(b)) == \
         (csl.INVALID_CHECKSUM, 0, int(ends[1500]))
     assert csl.validate_log(log, devices=devices)[:2] == (csl.SUCCESS, len(log))
+
+
+def test_gather_edges(cuda):
+    """bmqcrc_crc32c_gather edge cases: no buffers at all (every message the
+    seed), buffers outside [msg_first_buf[0], msg_first_buf[n]) ignored, one
+    buffer, a NULL pointer with length 0, and the Blob overload's seeds."""
+    from blazingmq_amd import _native as N
+    import ctypes
+
+    def run(bufs, first, seeds=None):
+        keep = [np.frombuffer(b, np.uint8) if b is not None else None for b in bufs]
+        ptrs = (ctypes.c_void_p * max(len(keep), 1))(
+            *[k.ctypes.data if k is not None and k.size else None for k in keep])
+        lens = np.array([0 if k is None else k.size for k in keep] or [0], np.uint32)
+        fb = np.asarray(first, np.uint64)
+        n = fb.size - 1
+        sd = None if seeds is None else np.asarray(seeds, np.uint32)
+        out = np.zeros(max(n, 1), np.uint32)
+        o = N.make_opts()
+        N.check(N.lib.bmqcrc_crc32c_gather(ptrs, lens.ctypes.data, len(bufs), fb.ctypes.data,
+                                           sd.ctypes.data if sd is not None else None,
+                                           out.ctypes.data, n, ctypes.byref(o)))
+        return out[:n].tolist()
+
+    assert run([], [0, 0, 0], seeds=[7, 0xFFFFFFFF]) == [7, 0xFFFFFFFF]
+    assert run([b"skip", b"hello world", b"skip too"], [1, 2]) == [oracle.crc32c(b"hello world")]
+    assert run([b"abc", None, b"def"], [0, 3], seeds=[5]) == [oracle.crc32c(b"abcdef", 5)]
+    assert run([b"x" * 5000], [0, 1, 1]) == [oracle.crc32c(b"x" * 5000), 0]
