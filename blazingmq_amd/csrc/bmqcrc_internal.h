@@ -22,11 +22,13 @@ constexpr int kBuckets = 16;            // segment size classes: floor(log2(line
 // Experiment knobs for same-box A/B builds (tools/build_variant.sh
 // -DBMQCRC_TUNE_BITS=...); the product is built with 0.  bit0 disables the
 // non-temporal LDS-DMA loads, bit1 forces a 1-block/CU k_fold grid, bit3
-// forces 2, bit4 always builds the size-class map (no shape prediction).
+// forces 2, bit4 always builds the size-class map (no shape prediction),
+// bit5 reads one- and two-line groups non-temporally too.
 #ifndef BMQCRC_TUNE_BITS
 #define BMQCRC_TUNE_BITS 0u
 #endif
 constexpr uint32_t kTuneBits = BMQCRC_TUNE_BITS;
+constexpr bool kShortDefaultPolicy = (kTuneBits & 32u) == 0;
 
 struct BatchArgs {
     const uint8_t* arena;      // device

@@ -822,10 +822,21 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         }
         setup_lane(valid, d.msg, d.k, nseg, d.off, d.len, d.seed, G);
     };
+    // Load policy per group: a group of one or two lines per lane (small
+    // messages) reads with the default policy, longer streams non-temporally.
+    // Measured on MI355X: the default policy is 3 %
+    // faster on 1M x 256 B and 8-10 % slower on every config of long streams.
     auto issue_first_rounds = [&](const Group& G) {
-        dma_round<NT>(wave_lds, G.pbase, G.plo, G.pcnt, zero, 0);
+        if (!NT || (kShortDefaultPolicy && G.R <= 2u)) {
+            dma_round<false>(wave_lds, G.pbase, G.plo, G.pcnt, zero, 0);
+            if (G.R > 1) {
+                dma_round<false>(wave_lds + kSlotBytes, G.pbase, G.plo, G.pcnt, zero, 1);
+            }
+            return;
+        }
+        dma_round<true>(wave_lds, G.pbase, G.plo, G.pcnt, zero, 0);
         if (G.R > 1) {
-            dma_round<NT>(wave_lds + kSlotBytes, G.pbase, G.plo, G.pcnt, zero, 1);
+            dma_round<true>(wave_lds + kSlotBytes, G.pbase, G.plo, G.pcnt, zero, 1);
         }
     };
 
