@@ -57,3 +57,53 @@ def test_fuzz_batch(cuda, round_):
     got = got.cpu().numpy().view(np.uint32)
     bad = np.nonzero(got != exp)[0]
     assert bad.size == 0, (round_, n, seg, whole, bad[:5], lens[bad[:5]], offs[bad[:5]])
+
+
+@pytest.mark.parametrize("round_", range(max(4, ROUNDS // 4)))
+def test_fuzz_gather(cuda, round_):
+    """bmqcrc_crc32c_gather on random Blob-shaped batches: buffer sizes from
+    the same distributions (including empty buffers and empty messages),
+    random message partitions, seeds -- against the oracle's Blob chain."""
+    import ctypes
+
+    from blazingmq_amd import _native as N
+    rng = np.random.default_rng(5000 + round_)
+    nbuf = int(rng.integers(0, 3000))
+    sizes = _lengths(rng, nbuf).astype(np.uint32) if nbuf else np.zeros(0, np.uint32)
+    bufs = [rng.integers(0, 256, size=int(k), dtype=np.uint8) for k in sizes]
+    n = int(rng.integers(1, 400))
+    first = np.sort(rng.integers(0, nbuf + 1, size=n + 1)).astype(np.uint64)
+    seeds = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+    ptrs = (ctypes.c_void_p * max(nbuf, 1))(*[b.ctypes.data if b.size else None for b in bufs])
+    lens = sizes if nbuf else np.zeros(1, np.uint32)
+    out = np.zeros(n, np.uint32)
+    o = N.make_opts()
+    N.check(N.lib.bmqcrc_crc32c_gather(ptrs, lens.ctypes.data, nbuf, first.ctypes.data,
+                                       seeds.ctypes.data, out.ctypes.data, n, ctypes.byref(o)))
+    exp = [oracle.blob([bufs[k].tobytes() for k in range(int(first[m]), int(first[m + 1]))],
+                       int(seeds[m])) for m in range(n)]
+    assert out.tolist() == exp
+
+
+@pytest.mark.parametrize("round_", range(max(3, ROUNDS // 8)))
+def test_fuzz_walks_over_devices(cuda, round_):
+    """Recovery verify of random partitions spread over 2-5 listings of the
+    device (bmqcrc_opts.ndevices) equals the single-device call: counts,
+    alarm offsets in order, bounded reports."""
+    from blazingmq_amd import storage
+    rng = np.random.default_rng(6000 + round_)
+    n = int(rng.integers(1, 3000))
+    apps = [rng.integers(0, 256, size=int(k), dtype=np.uint8).tobytes()
+            for k in _lengths(rng, n)]
+    j, d = storage.write_partition(apps)
+    for _ in range(int(rng.integers(0, 30))):
+        if d.size:
+            d[int(rng.integers(0, d.size))] ^= 0x20
+    one = storage.verify_partition(j, d)
+    for k in (2, 3, 5):
+        many = storage.verify_partition(j, d, devices=[0] * k)
+        assert (many["n_messages"], many["n_bad"]) == (one["n_messages"], one["n_bad"])
+        assert many["bad_record_offsets"].tolist() == one["bad_record_offsets"].tolist()
+        cap = int(rng.integers(0, 8))
+        assert storage.verify_partition(j, d, bad_cap=cap, devices=[0] * k)[
+            "bad_record_offsets"].tolist() == one["bad_record_offsets"][:cap].tolist()
