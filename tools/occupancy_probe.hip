@@ -54,6 +54,39 @@ __device__ __forceinline__ void issue(uint32_t lds_dst, const uint64_t (&s)[8])
 #undef OP
 }
 
+// A Horner-shaped chain of table lookups like k_fold's remainder step:
+// 16 steps x 8 lookups of 8-bit indices into eight 1 KiB tables (bank
+// conflicts as random bytes give them), or 16 steps x 16 lookups of 4-bit
+// indices into sixteen 64-byte tables (conflict-free: 16 entries = 16 banks,
+// equal addresses broadcast).  tab: LDS byte address of the tables.
+template <int KIND>
+__device__ __forceinline__ uint32_t horner_lookups(uint32_t c, uint32_t tab)
+{
+    typedef __attribute__((address_space(3))) uint32_t lds_u32;
+#pragma unroll
+    for (int d = 0; d < 16; ++d) {
+        const uint32_t v = c ^ (0x9E3779B9u * (uint32_t)(d + 1));
+        if (KIND == 1) {
+            uint32_t acc = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t b = (k < 4 ? v : (v * 0x85EBCA6Bu)) >> (8 * (k & 3)) & 0xffu;
+                acc ^= *(lds_u32*)(uintptr_t)(tab + 1024u * k + 4u * b);
+            }
+            c = acc;
+        } else {
+            uint32_t acc = 0;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const uint32_t b = (k < 8 ? v : (v * 0x85EBCA6Bu)) >> (4 * (k & 7)) & 0xfu;
+                acc ^= *(lds_u32*)(uintptr_t)(tab + 64u * k + 4u * b);
+            }
+            c = acc;
+        }
+    }
+    return c;
+}
+
 __device__ __forceinline__ void work4(uint32_t (&v)[4], uint32_t work)
 {
     for (uint32_t k = 0; k < work; k += 16) {
@@ -68,7 +101,7 @@ __device__ __forceinline__ void work4(uint32_t (&v)[4], uint32_t work)
 }
 
 // HALF: rounds of 64 B per lane; ROUNDS per group = 2 lines * (HALF ? 2 : 1)
-template <bool NT, int HALF, int BPC>
+template <bool NT, int HALF, int BPC, int KIND = 0>
 __global__ __launch_bounds__(256, BPC) void probe(const uint8_t* base, uint64_t ngroups,
                                                    uint32_t work, uint32_t* sink)
 {
@@ -79,7 +112,7 @@ __global__ __launch_bounds__(256, BPC) void probe(const uint8_t* base, uint64_t 
     constexpr uint32_t kLanesPerPiece = HALF == 1 ? 4u : 8u;  // lanes sharing one 64/128 B unit
     constexpr uint32_t kRounds = HALF == 1 ? 4u : 2u;
     constexpr uint32_t kRoundBytes = HALF == 1 ? 64u : 128u;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[4 * 2 * kSlot];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[4 * 2 * kSlot + 8192];
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wl = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)lds +
@@ -122,27 +155,35 @@ __global__ __launch_bounds__(256, BPC) void probe(const uint8_t* base, uint64_t 
                 issue<NT, kInstr>(slot, s);
             }
         }
-        work4(v, work);
+        if (KIND == 0) {
+            work4(v, work);
+        } else {
+            const uint32_t tab = (uint32_t)(uintptr_t)(
+                __attribute__((address_space(3))) uint8_t*)lds + 4u * 2u * kSlot;
+            for (uint32_t k = 0; k < work; k += 400u) {  // one remainder-step chain per 400
+                v[1] = horner_lookups<KIND>(v[1] ^ v[0], tab);
+            }
+        }
     }
     if ((v[0] ^ v[1] ^ v[2] ^ v[3]) == 0x12345678u) {
         sink[0] = 1;
     }
 }
 
-template <bool NT, int HALF, int BPC>
+template <bool NT, int HALF, int BPC, int KIND = 0>
 void run(const uint8_t* buf, uint64_t bytes, uint32_t work, uint32_t* sink, int cus,
          hipEvent_t a, hipEvent_t b)
 {
     const uint64_t ngroups = bytes / (64ull * 256u);
     const int grid = BPC * cus;
     for (int w = 0; w < 3; ++w) {
-        hipLaunchKernelGGL((probe<NT, HALF, BPC>), dim3(grid), dim3(256), 0, 0, buf, ngroups, work,
+        hipLaunchKernelGGL((probe<NT, HALF, BPC, KIND>), dim3(grid), dim3(256), 0, 0, buf, ngroups, work,
                            sink);
     }
     const int reps = 20;
     hipEventRecord(a, 0);
     for (int r = 0; r < reps; ++r) {
-        hipLaunchKernelGGL((probe<NT, HALF, BPC>), dim3(grid), dim3(256), 0, 0, buf, ngroups, work,
+        hipLaunchKernelGGL((probe<NT, HALF, BPC, KIND>), dim3(grid), dim3(256), 0, 0, buf, ngroups, work,
                            sink);
     }
     hipEventRecord(b, 0);
@@ -150,9 +191,9 @@ void run(const uint8_t* buf, uint64_t bytes, uint32_t work, uint32_t* sink, int 
     float ms = 0;
     hipEventElapsedTime(&ms, a, b);
     const double us = 1000.0 * ms / reps;
-    printf("{\"mode\": %d, \"waves_per_simd\": %d, \"nt\": %d, \"work\": %u, "
+    printf("{\"mode\": %d, \"waves_per_simd\": %d, \"nt\": %d, \"work\": %u, \"kind\": %d, "
            "\"us\": %.2f, \"TBps\": %.3f}\n",
-           HALF, BPC, NT ? 1 : 0, work, us, bytes / us / 1e6);
+           HALF, BPC, NT ? 1 : 0, work, KIND, us, bytes / us / 1e6);
     fflush(stdout);
 }
 
@@ -169,13 +210,12 @@ int main()
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    for (uint32_t work : {0u, 400u, 800u}) {
-        run<true, 0, 2>(buf, bytes, work, sink, cus, a, b);
-        run<false, 0, 2>(buf, bytes, work, sink, cus, a, b);
-        run<true, 2, 2>(buf, bytes, work, sink, cus, a, b);
-        run<false, 2, 2>(buf, bytes, work, sink, cus, a, b);
-        run<false, 1, 3>(buf, bytes, work, sink, cus, a, b);
-        run<false, 1, 4>(buf, bytes, work, sink, cus, a, b);
+    // kind 0: VALU chains; 1: byte-table Horner (128 lookups per 400); 2: nibble tables (256)
+    for (uint32_t work : {400u, 800u}) {
+        run<false, 0, 2, 0>(buf, bytes, work, sink, cus, a, b);
+        run<false, 0, 2, 1>(buf, bytes, work, sink, cus, a, b);
+        run<false, 0, 2, 2>(buf, bytes, work, sink, cus, a, b);
     }
+    run<false, 0, 2, 0>(buf, bytes, 0, sink, cus, a, b);
     return 0;
 }
