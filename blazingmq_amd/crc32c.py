@@ -100,9 +100,11 @@ class Crc32c:
         return _native.lib.bmqcrc_combine(crc_a & 0xFFFFFFFF, crc_b & 0xFFFFFFFF, len_b)
 
     @staticmethod
-    def verify_batch(arena, offsets, lengths, expected, bad_cap=1 << 20, seg_bytes=0):
+    def verify_batch(arena, offsets, lengths, expected, bad_cap=1 << 20, seg_bytes=0,
+                     devices=None):
         """Batched recovery check (bmqcrc_crc32c_verify): (n_bad, bad indices)."""
-        return verify_batch(arena, offsets, lengths, expected, bad_cap, seg_bytes)
+        return verify_batch(arena, offsets, lengths, expected, bad_cap, seg_bytes,
+                            devices=devices)
 
     @staticmethod
     def calculate_blobs(blobs, seeds=None, seg_bytes=0, gather=True):
@@ -112,7 +114,7 @@ class Crc32c:
     @staticmethod
     def calculate_batch(arena, offsets, lengths, seeds=None, out=None, *, seg_bytes=0,
                         device=None, stream=None, sync=True, time_kernel=False,
-                        whole_messages=False):
+                        whole_messages=False, devices=None):
         """Batched CRC32-C of messages ``arena[offsets[i] : offsets[i]+lengths[i]]``.
 
         torch CUDA tensors: ``arena`` uint8, ``offsets`` int64, ``lengths`` /
@@ -121,6 +123,7 @@ class Crc32c:
         ``out`` (int32 tensor) is returned.  Host arrays: numpy in, numpy
         ``uint32`` out.  ``whole_messages`` (BMQCRC_F_WHOLE_MESSAGES): one
         lane per message, no planner launches -- for batches of small messages.
+        ``devices`` (host arrays only): split the batch over several GPUs.
         """
         try:
             import torch
@@ -130,7 +133,7 @@ class Crc32c:
             return _batch_torch(torch, arena, offsets, lengths, seeds, out, seg_bytes, stream,
                                 sync, time_kernel, whole_messages)
         return _batch_host(arena, offsets, lengths, seeds, out, seg_bytes, device,
-                           whole_messages)
+                           whole_messages, devices)
 
 
 def _batch_torch(torch, arena, offsets, lengths, seeds, out, seg_bytes, stream, sync,
@@ -179,7 +182,8 @@ def _check_host_out(out, n):
     return out
 
 
-def _batch_host(arena, offsets, lengths, seeds, out, seg_bytes, device, whole_messages=False):
+def _batch_host(arena, offsets, lengths, seeds, out, seg_bytes, device, whole_messages=False,
+                devices=None):
     a = np.frombuffer(bytes(arena), dtype=np.uint8) if isinstance(
         arena, (bytes, bytearray, memoryview)) else np.ascontiguousarray(arena).view(np.uint8)
     off = np.ascontiguousarray(offsets, dtype=np.uint64)
@@ -191,7 +195,8 @@ def _batch_host(arena, offsets, lengths, seeds, out, seg_bytes, device, whole_me
         raise ValueError("seeds must have one entry per message")
     res = np.empty(off.size, dtype=np.uint32) if out is None else _check_host_out(out, off.size)
     o = _native.make_opts(device=-1 if device is None else device, seg_bytes=seg_bytes,
-                          flags=_native.BMQCRC_F_WHOLE_MESSAGES if whole_messages else 0)
+                          flags=_native.BMQCRC_F_WHOLE_MESSAGES if whole_messages else 0,
+                          devices=devices)
     _native.check(_native.lib.bmqcrc_crc32c_batch(
         a.ctypes.data if a.size else None, a.size, off.ctypes.data, ln.ctypes.data,
         sd.ctypes.data if sd is not None else None, res.ctypes.data, off.size, ctypes.byref(o)))
@@ -204,7 +209,8 @@ def _u8_host(arena):
     return np.ascontiguousarray(arena).view(np.uint8).reshape(-1)
 
 
-def verify_batch(arena, offsets, lengths, expected, bad_cap=1 << 20, seg_bytes=0, device=None):
+def verify_batch(arena, offsets, lengths, expected, bad_cap=1 << 20, seg_bytes=0, device=None,
+                 devices=None):
     """GPU batch CRC of every message compared on the device with `expected`.
 
     Returns (n_bad, bad_index ndarray[uint64], ascending, at most bad_cap)."""
@@ -216,7 +222,8 @@ def verify_batch(arena, offsets, lengths, expected, bad_cap=1 << 20, seg_bytes=0
         raise ValueError("offsets/lengths/expected size mismatch")
     nbad = ctypes.c_uint64()
     idx = np.zeros(max(int(bad_cap), 1), dtype=np.uint64)
-    o = _native.make_opts(device=-1 if device is None else device, seg_bytes=seg_bytes)
+    o = _native.make_opts(device=-1 if device is None else device, seg_bytes=seg_bytes,
+                          devices=devices)
     _native.check(_native.lib.bmqcrc_crc32c_verify(
         a.ctypes.data if a.size else None, a.size, off.ctypes.data, ln.ctypes.data,
         ex.ctypes.data, off.size, ctypes.byref(nbad), idx.ctypes.data, int(bad_cap),

@@ -499,6 +499,31 @@ int verify_locked(Ctx& c, Workspace* w, const bmqcrc_opts& o, uint32_t seg, bool
                   const uint32_t* lengths, const uint32_t* expected, uint64_t n, uint64_t* n_bad,
                   uint64_t* bad_idx, uint64_t bad_cap, uint64_t* n_written);
 
+int verify_host_multi(const void* arena, uint64_t arena_bytes, bmqcrc_prepare_fn prepare,
+                      void* pctx, uint64_t* n_bad, std::vector<uint64_t>* bad, uint64_t bad_cap,
+                      const bmqcrc_opts& o, uint32_t seg, std::vector<uint32_t>* crcs,
+                      uint64_t* n_written);
+
+// The message arrays of a plain verify call, handed to verify_host_multi as
+// an already finished "walk".
+struct GivenArrays {
+    const uint64_t* off;
+    const uint32_t* len;
+    const uint32_t* exp;
+    uint64_t n;
+};
+
+int given_arrays(void* ctx, const uint64_t** off, const uint32_t** len, const uint32_t** exp,
+                 uint64_t* n)
+{
+    const GivenArrays* g = (const GivenArrays*)ctx;
+    *off = g->off;
+    *len = g->len;
+    *exp = g->exp;
+    *n = g->n;
+    return 0;
+}
+
 }  // namespace
 
 extern "C" int bmqcrc_set_error(int rc, const char* msg)
@@ -557,6 +582,10 @@ int bmqcrc_crc32c_batch(const void* arena, uint64_t arena_bytes, const uint64_t*
     if (!(o.flags & BMQCRC_F_DEVICE_PTRS) && (rc = check_ranges(offsets, lengths, n, arena_bytes))) {
         return rc;  // device arrays are trusted
     }
+    if (!(o.flags & BMQCRC_F_DEVICE_PTRS) && o.ndevices > 1) {  // one byte range per device
+        return bmqcrc_crc32c_batch_multi(arena, arena_bytes, offsets, lengths, seeds, out, n,
+                                         o.devices, (int)o.ndevices, seg);
+    }
     return batch_one(dev, o.stream, o.flags, seg, arena, arena_bytes, offsets, lengths, seeds,
                      out, n);
 }
@@ -590,6 +619,17 @@ int bmqcrc_crc32c_verify(const void* arena, uint64_t arena_bytes, const uint64_t
     const bool dev_ptrs = (o.flags & BMQCRC_F_DEVICE_PTRS) != 0;
     if (!dev_ptrs && (rc = check_ranges(offsets, lengths, n, arena_bytes))) {
         return rc;
+    }
+    if (!dev_ptrs && o.ndevices > 1) {  // one byte range per device, merged in index order
+        GivenArrays ga = {offsets, lengths, expected, n};
+        std::vector<uint64_t> bad;
+        uint64_t written = 0;
+        if ((rc = verify_host_multi(arena, arena_bytes, given_arrays, &ga, n_bad, &bad, bad_cap, o,
+                                    seg, nullptr, &written))) {
+            return rc;
+        }
+        std::copy(bad.begin(), bad.begin() + written, bad_idx);
+        return 0;
     }
     Ctx c;
     if ((rc = open_ctx(dev, o.stream, &c))) {

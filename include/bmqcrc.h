@@ -63,13 +63,15 @@ typedef struct bmqcrc_opts {
     uint32_t flags;       /* BMQCRC_F_* */
     uint32_t seg_bytes;   /* segment size in bytes, multiple of 128 in [256, 2^30]; 0 = automatic
                              from the batch's size (256 B - 64 KiB) */
-    /* ABI 2.1.  Format-walk entry points (bmqcrc_protocol.h: recovery verify,
-     * PUT-event fill/verify, ledger validate) only: with ndevices > 1 the
-     * input buffer is cut into ndevices contiguous byte ranges, each copied to
-     * its own device (its own PCIe link) while the calling thread walks the
-     * format; each device then verifies the messages lying in its range, and
-     * the few that straddle a cut are done by the first device.  Results are
-     * identical to the single-device call.  devices == NULL means
+    /* ABI 2.1.  Host-buffer calls only (bmqcrc_crc32c_batch, bmqcrc_crc32c_verify
+     * and the format walks of bmqcrc_protocol.h: recovery verify, PUT-event
+     * fill/verify, ledger validate): with ndevices > 1 the input is split over
+     * ndevices devices, each copying its part over its own PCIe link.  The
+     * batch splits the messages byte-balanced (bmqcrc_crc32c_batch_multi);
+     * verify and the walks cut the buffer into contiguous byte ranges, copied
+     * while the calling thread walks the format, each device verifies the
+     * messages lying in its range and the few that straddle a cut are done by
+     * the first device.  Results are identical to the single-device call.  devices == NULL means
      * 0..ndevices-1; a device may be listed more than once (each listing gets
      * a library-owned stream); `device` and `stream` are then ignored.
      * ndevices 0 or 1: the single device above.  Callers built against ABI

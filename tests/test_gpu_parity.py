@@ -502,3 +502,27 @@ def test_ranks_shard_a_batch_on_the_gpu(cuda):
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "bit_exact=True" in r.stdout
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0, 0, 0]])
+def test_host_batch_and_verify_over_device_listings(cuda, devices):
+    """bmqcrc_opts.ndevices on the plain host-buffer calls: the batch splits
+    its messages byte-balanced over the listings, verify cuts the arena into
+    ranges (straddling messages on the first listing); both equal the
+    one-device call and the oracle, bounded reports included."""
+    rng = np.random.default_rng(23)
+    arena = rng.integers(0, 256, size=6 << 20, dtype=np.uint8)
+    lens = rng.integers(0, 90000, size=700).astype(np.uint32)
+    offs = np.array([rng.integers(0, arena.size - l + 1) for l in lens], dtype=np.uint64)
+    seeds = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64).astype(np.uint32)
+    exp = oracle.batch(arena, offs, lens, seeds, nthreads=8)
+    got = Crc32c.calculate_batch(arena, offs, lens, seeds, devices=devices)
+    assert np.array_equal(got, exp)
+    plain = oracle.batch(arena, offs, lens, nthreads=8)
+    wrong = plain.copy()
+    victims = sorted(set(int(i) for i in rng.integers(0, lens.size, size=23)))
+    wrong[victims] ^= 1
+    n_bad, bad = Crc32c.verify_batch(arena, offs, lens, wrong, devices=devices)
+    assert n_bad == len(victims) and bad.tolist() == victims
+    n_bad, bad = Crc32c.verify_batch(arena, offs, lens, wrong, bad_cap=5, devices=devices)
+    assert n_bad == len(victims) and bad.tolist() == victims[:5]
