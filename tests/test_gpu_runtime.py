@@ -132,3 +132,49 @@ def test_default_stream_ordering(cuda):
         torch.cuda.default_stream(cuda).synchronize()
     exp = oracle.batch(arena.cpu().numpy(), offs, lens, nthreads=8)
     assert np.array_equal(host.numpy().view(np.uint32), exp)
+
+
+def test_concurrent_gather_and_multi_device_walks(cuda):
+    """Host-buffer calls from several threads at once: Blob gathers (the
+    default stream's workspace and its pinned ring) and recovery walks spread
+    over 2 and 3 listings of the device (library-owned streams shared between
+    the calls) -- no deadlock, every result equal to a serial call."""
+    from blazingmq_amd import Blob, storage
+    rng = np.random.default_rng(42)
+    apps = [rng.integers(0, 256, size=int(k), dtype=np.uint8).tobytes()
+            for k in rng.integers(0, 40000, size=1500)]
+    j, d = storage.write_partition(apps)
+    for i in rng.integers(0, d.size, size=9):
+        d[int(i)] ^= 0x08
+    serial = storage.verify_partition(j, d)
+    blobs = [Blob([rng.integers(0, 256, size=int(k), dtype=np.uint8).tobytes()
+                   for k in rng.integers(0, 9000, size=int(rng.integers(0, 9)))])
+             for _ in range(300)]
+    blob_exp = Crc32c.calculate_blobs(blobs).tolist()
+    errors = []
+
+    def walks(devs):
+        try:
+            for _ in range(6):
+                r = storage.verify_partition(j, d, devices=devs)
+                assert r["n_bad"] == serial["n_bad"]
+                assert r["bad_record_offsets"].tolist() == serial["bad_record_offsets"].tolist()
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    def gathers():
+        try:
+            for _ in range(6):
+                assert Crc32c.calculate_blobs(blobs).tolist() == blob_exp
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    threads = [threading.Thread(target=walks, args=([0, 0],)),
+               threading.Thread(target=walks, args=([0, 0, 0],)),
+               threading.Thread(target=gathers), threading.Thread(target=gathers)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=150)
+    assert not any(th.is_alive() for th in threads), "a host-buffer call did not return"
+    assert not errors, errors
