@@ -1141,19 +1141,16 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
             load(base + kTile, nxt, nxo);  // next tile in flight during this scan
         }
         if (classes) {
-            // class of each message's last (or only) segment, one LDS atomic
-            // per class and wave
+            // class of each message's last (or only) segment: one
+            // returnless LDS atomic per message (a ballot and a conditional
+            // atomic per class and wave measured 43 against 26 us on Zipf 4M)
 #pragma unroll
             for (uint32_t v = 0; v < kPlanV; ++v) {
                 uint32_t c;
                 const uint32_t nseg = msg_segments(a, O[v], L[v], seg_shift, &c);
                 full += nseg ? nseg - 1u : 0u;
-#pragma unroll
-                for (int cc = 0; cc < kBuckets; ++cc) {
-                    const uint64_t m = __ballot(c == (uint32_t)cc);
-                    if (m && lane == 0) {
-                        atomicAdd(&hist[cc], (uint32_t)__popcll(m));
-                    }
+                if (c < (uint32_t)kBuckets) {
+                    atomicAdd(&hist[c], 1u);
                 }
             }
         }
@@ -1267,6 +1264,12 @@ __device__ __forceinline__ void load_tile(const BatchArgs& a, uint64_t base, uin
 // Positions inside a block's slice are claimed with wave-aggregated LDS
 // atomics: the order within a bucket may differ between runs, the CRCs do not
 // (XOR combine).
+// Runs of at most kShortRun full segments are written by their own lane
+// (one claim each); longer runs by the whole wave, lane by lane.  Zipf 4M:
+// 61.5 us with every run walked by the wave, 52 with 4-segment short runs,
+// 49.5 with 8, 51.4 with 16 (same-box A/B, profiles/r02/ab/).
+constexpr uint32_t kShortRun = 8u;
+
 __global__ __launch_bounds__(kPlanBlock) void k_plan_sort(BatchArgs a)
 {
     __shared__ uint32_t run[kBuckets];
@@ -1315,7 +1318,6 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_sort(BatchArgs a)
     const uint32_t SEG = a.seg_bytes;
     const uint32_t seg_shift = (SEG & (SEG - 1u)) == 0 ? (uint32_t)__builtin_ctz(SEG) : 0u;
     const uint32_t c_full = size_class(SEG >> 7);
-    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint2* const info = (uint2*)a.seginfo;
     const uint64_t lo = (uint64_t)blockIdx.x * a.per_msg;
     const uint64_t hi = min(lo + a.per_msg, a.n);
@@ -1333,10 +1335,20 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_sort(BatchArgs a)
 #pragma unroll
         for (uint32_t v = 0; v < kPlanV; ++v) {
             nseg[v] = msg_segments(a, cur.off[v], cur.len[v], seg_shift, &c[v]);
-            nf_all += nseg[v] ? nseg[v] - 1u : 0u;
+            const uint32_t nf = nseg[v] ? nseg[v] - 1u : 0u;
+            if (nf && nf <= kShortRun) {
+                // a short run of full segments: its lane claims and writes it
+                const uint32_t at = atomicAdd(&run[c_full], nf);
+                const uint32_t i = (uint32_t)(base + (uint64_t)v * kPlanBlock + threadIdx.x);
+                for (uint32_t k = 0; k < nf; ++k) {
+                    info[at + k] = make_uint2(i, k);
+                }
+            } else {
+                nf_all += nf;
+            }
         }
-        // non-last segments: one contiguous run per message in class c_full,
-        // one LDS atomic per wave and tile
+        // long runs of full segments: one contiguous run per message in class
+        // c_full, one LDS atomic per wave and tile
         uint32_t x = nf_all;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -1361,8 +1373,9 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_sort(BatchArgs a)
                 uint32_t at = (uint32_t)__builtin_amdgcn_readlane((int)pos, src);
 #pragma unroll
                 for (uint32_t v = 0; v < kPlanV; ++v) {
+                    const uint32_t nfv = nseg[v] ? nseg[v] - 1u : 0u;
                     const uint32_t nf = (uint32_t)__builtin_amdgcn_readlane(
-                        (int)(nseg[v] ? nseg[v] - 1u : 0u), src);
+                        (int)(nfv > kShortRun ? nfv : 0u), src);
                     const uint32_t i =
                         (uint32_t)(base + (uint64_t)v * kPlanBlock + lane0 + (uint32_t)src);
                     for (uint32_t k = (uint32_t)lane; k < nf; k += 64u) {
@@ -1372,31 +1385,15 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_sort(BatchArgs a)
                 }
             }
         }
-        // last (or only) segments: per class, one LDS atomic per wave and tile
+        // last (or only) segments: a returning LDS atomic per message claims
+        // its slot in its class (the order inside a bucket is free; a ballot,
+        // an atomic and a shuffle per class and wave measured 73 against 61 us
+        // on Zipf 4M)
 #pragma unroll
-        for (int cc = 0; cc < kBuckets; ++cc) {
-            uint64_t m[kPlanV];
-            uint32_t tot = 0;
-#pragma unroll
-            for (uint32_t v = 0; v < kPlanV; ++v) {
-                m[v] = __ballot(c[v] == (uint32_t)cc);
-                tot += (uint32_t)__popcll(m[v]);
-            }
-            if (tot) {
-                uint32_t p = 0;
-                if (lane == 0) {
-                    p = atomicAdd(&run[cc], tot);
-                }
-                p = (uint32_t)__shfl((int)p, 0);
-#pragma unroll
-                for (uint32_t v = 0; v < kPlanV; ++v) {
-                    if (c[v] == (uint32_t)cc) {
-                        const uint64_t i = base + (uint64_t)v * kPlanBlock + threadIdx.x;
-                        info[p + (uint32_t)__popcll(m[v] & below)] =
-                            make_uint2((uint32_t)i, nseg[v] - 1u);
-                    }
-                    p += (uint32_t)__popcll(m[v]);
-                }
+        for (uint32_t v = 0; v < kPlanV; ++v) {
+            if (c[v] < (uint32_t)kBuckets) {
+                const uint64_t i = base + (uint64_t)v * kPlanBlock + threadIdx.x;
+                info[atomicAdd(&run[c[v]], 1u)] = make_uint2((uint32_t)i, nseg[v] - 1u);
             }
         }
     }
