@@ -374,11 +374,19 @@ int run_batch(Ctx& c, uint32_t flags, uint32_t seg, const void* arena, uint64_t 
         return rc;
     } else if (!(kTuneBits & 16u)) {
         const uint32_t hint = __atomic_load_n(w->hint_host, __ATOMIC_RELAXED);
-        if (hint == kHintClosed || hint == kHintIdentity) {
+        const uint32_t shape = hint & 0xffu, hint_u = hint >> 8;
+        if (shape == kHintClosed || shape == kHintIdentity) {
             a.map_planned = 0;  // last batch was closed-form: predict this one is too
         }
-        if (hint == kHintIdentity && spec_eligible(c, n, a.blocks_per_cu)) {
+        if (shape == kHintIdentity && spec_eligible(c, n, a.blocks_per_cu)) {
             a.spec = 1;  // ... and one segment per message: one launch, no planner
+        } else if (shape == kHintClosed && hint_u >= 2u && hint_u <= 64u && 64u % hint_u == 0u &&
+                   (uint64_t)n * hint_u <= 0xFFFFFF00ull) {
+            // ... and the same u segments per message, u dividing 64: every
+            // group holds 64/u whole messages, so one launch needs no planner
+            // and no cross-group combine (a message of another count is folded
+            // by its wave's second pass, and the next batch is planned again)
+            a.spec = hint_u;
         }
     }
     if (!a.whole && host_max_len <= a.seg_bytes) {

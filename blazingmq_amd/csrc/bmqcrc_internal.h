@@ -57,16 +57,18 @@ struct BatchArgs {
     uint32_t* shape_hint;      // host-mapped word or nullptr: k_fold writes kHintIdentity,
                                // kHintClosed or kHintRagged, the host reads it when planning
                                // the next batch
-    // Speculative single launch (spec = 1): the previous batch on this
-    // workspace had one segment per message, so no planner runs and k_fold
-    // folds message g in lane g.  A message longer than one segment is
-    // skipped there and folded by the same wave afterwards, 64 segments at a
-    // time -- correct for any batch, only slower when the guess was wrong.
+    // Speculative single launch (spec = u > 0): the previous batch on this
+    // workspace had u segments per message (u = 1, or u dividing 64), so no
+    // planner runs and k_fold folds segment k of message m in slot m*u + k
+    // (a group holds 64/u whole messages).  A message with another segment
+    // count is skipped there and folded by the same wave afterwards, 64
+    // segments at a time -- correct for any batch, only slower when the
+    // guess was wrong.
     uint32_t spec;
 };
 
 constexpr uint32_t kHintUnknown = 0;
-constexpr uint32_t kHintClosed = 1;  // uniform segment counts (> 1)
+constexpr uint32_t kHintClosed = 1;  // uniform segment counts (> 1); | (u << 8) when u divides 64
 constexpr uint32_t kHintRagged = 2;
 constexpr uint32_t kHintIdentity = 3;  // one segment per message
 

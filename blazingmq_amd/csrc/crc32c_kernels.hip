@@ -689,7 +689,10 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         tw[i] = c_ty[t >> 8][t & 255u];
     }
     const uint32_t whole = a.whole;
-    const uint32_t spec_mode = a.spec;  // speculative single launch: no planner ran
+    // speculative single launch (no planner ran): every message predicted to
+    // have spec_u segments, spec_u dividing 64 (1: one segment per message)
+    const uint32_t spec_mode = a.spec;
+    const uint32_t spec_u = spec_mode ? spec_mode : 1u;
     PlanWords pw = {0u, 0u, 0u, 0u};
     if (!whole && !spec_mode) {
         pw = plan_load(a);
@@ -713,10 +716,12 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     }
 
     // BMQCRC_F_WHOLE_MESSAGES and speculative launches: group g = messages
-    // 64g..64g+63, no planner ran.  Otherwise the batch totals come from
-    // k_plan's block words.
+    // 64g..64g+63 (speculative uniform: 64g/u .. 64(g+1)/u - 1, u segments
+    // each), no planner ran.  Otherwise the batch totals come from k_plan's
+    // block words.
     __shared__ PlanLds pl;
-    PlanTotals pt = {(uint32_t)a.n, 1u, 0u, 0u};
+    PlanTotals pt = {(uint32_t)a.n * spec_u, spec_u == 1u ? 1u : 0u, spec_u == 1u ? 0u : spec_u,
+                     0u};
     if (!whole && !spec_mode) {
         pt = plan_reduce(a, &pl, pw);
     } else {
@@ -740,10 +745,13 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     if (a.shape_hint && blockIdx.x == 0 && threadIdx.x == 0 && !whole && !spec_mode) {
         // batch shape for the host's next launch decision (host-mapped word);
         // a speculative launch keeps kHintIdentity unless a message is queued
+        // (a closed-form batch whose u segments per message divide 64 also
+        // records u: its successor can run speculatively, see kHintClosed)
         __hip_atomic_store(a.shape_hint,
                            (identity && !pt.overflow) ? kHintIdentity
-                                                      : (uni || pt.overflow) ? kHintClosed
-                                                                             : kHintRagged,
+                           : (uni && !pt.overflow && 64u % uni == 0u) ? (kHintClosed | (uni << 8))
+                           : (uni || pt.overflow) ? kHintClosed
+                                                  : kHintRagged,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 
@@ -814,11 +822,13 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         bool valid = seg < total;
         uint32_t nseg = !valid ? 0u : (wholef ? 1u : segments(d.len));
         if (spec_mode) {
-            // a message longer than one segment is left to the wave's second
-            // pass (below); an empty message is folded whole (its seed)
-            long_seen |= __ballot(valid && nseg > 1u) != 0;
-            valid = valid && nseg <= 1u;
-            nseg = 1u;
+            // a message of another segment count than predicted is left to
+            // the wave's second pass (below); with u = 1 an empty message is
+            // folded whole (its seed)
+            const bool ok = spec_u == 1u ? nseg <= 1u : nseg == spec_u;
+            long_seen |= __ballot(valid && !ok) != 0;
+            valid = valid && ok;
+            nseg = spec_u;
         }
         setup_lane(valid, d.msg, d.k, nseg, d.off, d.len, d.seed, G);
     };
@@ -960,18 +970,21 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     // wave runs this pass.
     auto second_pass = [&]() {
         bool any = false;
+        const uint32_t mpg = 64u / spec_u;  // messages per group
         for (uint32_t gg = g0; gg < ngroups; gg += stride) {
-            const uint32_t i = gg * 64u + (uint32_t)lane;
-            const uint32_t len = i < a.n ? a.lengths[i] : 0u;
-            uint64_t todo = __ballot(segments(len) > 1u);
+            const uint64_t i = (uint64_t)gg * mpg + (uint32_t)lane;
+            const bool mine = (uint32_t)lane < mpg && i < a.n;
+            const uint32_t len = mine ? a.lengths[i] : 0u;
+            const uint32_t ns = segments(len);
+            uint64_t todo = __ballot(mine && (spec_u == 1u ? ns > 1u : ns != spec_u));
             any = any || todo != 0;
             for (; todo; todo &= todo - 1ull) {
-                const uint32_t msg = gg * 64u + (uint32_t)__builtin_ctzll(todo);
+                const uint32_t msg = (uint32_t)((uint64_t)gg * mpg + __builtin_ctzll(todo));
                 const uint64_t off = a.offsets[msg];
                 const uint32_t mlen = a.lengths[msg];
                 const uint32_t seed = a.seeds ? a.seeds[msg] : 0u;
                 const uint32_t nseg = segments(mlen);
-                uint32_t acc = 0;
+                uint32_t acc = mlen ? 0u : seed;  // an empty message's CRC is its seed
                 for (uint32_t c = 0; 64u * c < nseg; ++c) {
                     const uint32_t k = 64u * c + (uint32_t)lane;
                     Group H;

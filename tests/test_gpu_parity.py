@@ -526,3 +526,47 @@ def test_host_batch_and_verify_over_device_listings(cuda, devices):
     assert n_bad == len(victims) and bad.tolist() == victims
     n_bad, bad = Crc32c.verify_batch(arena, offs, lens, wrong, bad_cap=5, devices=devices)
     assert n_bad == len(victims) and bad.tolist() == victims[:5]
+
+
+def test_speculative_uniform_launch(cuda):
+    """After a batch of u segments per message with u dividing 64, the next
+    batch on the stream is ONE k_fold launch (BatchArgs::spec = u): a group
+    holds 64/u whole messages.  Messages of another segment count (shorter,
+    longer, empty, thousands of segments) are folded by their wave's second
+    pass; every batch of the sequence is bit-exact, including u = 3 (not a
+    divisor of 64: planned as before) and batches smaller than the grid."""
+    import torch
+    rng = np.random.default_rng(79)
+    arena_np = rng.integers(0, 256, size=64 << 20, dtype=np.uint8)
+    arena = torch.from_numpy(arena_np).to(cuda)
+    s = torch.cuda.Stream(cuda)
+    seg = 1024
+
+    def run(lens, tag):
+        lens = np.asarray(lens, np.uint32)
+        offs = np.array(rng.integers(0, arena_np.size - lens.astype(np.int64) + 1), np.int64)
+        seeds = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64).astype(np.uint32)
+        seeds[::4] = 0
+        got = Crc32c.calculate_batch(arena, torch.from_numpy(offs).to(cuda),
+                                     torch.from_numpy(lens.view(np.int32)).to(cuda),
+                                     torch.from_numpy(seeds.view(np.int32)).to(cuda),
+                                     stream=s, seg_bytes=seg)
+        s.synchronize()
+        exp = oracle.batch(arena_np, offs, lens, seeds, nthreads=8)
+        bad = np.nonzero(got.cpu().numpy().view(np.uint32) != exp)[0]
+        assert bad.size == 0, (tag, [(int(i), int(lens[i])) for i in bad[:8]])
+
+    def uniform(u, n):  # lengths of exactly u segments of seg bytes
+        return rng.integers((u - 1) * seg + 1, u * seg + 1, size=n)
+
+    for u, n in ((4, 50_000), (16, 1_000), (64, 3_000), (2, 200_000)):
+        run(uniform(u, n), "planned u=%d" % u)
+        run(uniform(u, n), "spec u=%d" % u)
+        odd = uniform(u, n)
+        where = rng.integers(0, n, size=max(8, n // 500))
+        odd[where] = rng.choice([0, 1, seg, (u + 1) * seg, 100 * seg], size=where.size)
+        odd[-1] = 3 << 20  # thousands of segments, in the last group
+        run(odd, "spec mispredicted u=%d" % u)
+        run(uniform(u, n), "planned again u=%d" % u)
+    run(uniform(3, 30_000), "u=3")
+    run(uniform(3, 30_000), "u=3 again (not speculative)")
