@@ -667,7 +667,10 @@ __device__ __forceinline__ SegDesc fetch_desc(const BatchArgs& a, SegRef r, bool
     return d;
 }
 
-template <bool NT>
+// ONE: a speculative launch predicting one segment per message (spec == 1),
+// compiled apart so the first pass knows k = 0 and nseg = 1 (no planner words,
+// no move to the message end, no run combine).
+template <bool NT, bool ONE>
 __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kTabBytes + kLdsBytes];
@@ -688,10 +691,10 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         const uint32_t t = threadIdx.x + (uint32_t)i * (kWavesPerBlock * 64);
         tw[i] = c_ty[t >> 8][t & 255u];
     }
-    const uint32_t whole = a.whole;
+    const uint32_t whole = ONE ? 0u : a.whole;
     // speculative single launch (no planner ran): every message predicted to
     // have spec_u segments, spec_u dividing 64 (1: one segment per message)
-    const uint32_t spec_mode = a.spec;
+    const uint32_t spec_mode = ONE ? 1u : a.spec;
     const uint32_t spec_u = spec_mode ? spec_mode : 1u;
     PlanWords pw = {0u, 0u, 0u, 0u};
     if (!whole && !spec_mode) {
@@ -830,7 +833,11 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
             valid = valid && ok;
             nseg = spec_u;
         }
-        setup_lane(valid, d.msg, d.k, nseg, d.off, d.len, d.seed, G);
+        if (ONE) {
+            setup_lane(valid, d.msg, 0u, 1u, d.off, d.len, d.seed, G);
+        } else {
+            setup_lane(valid, d.msg, d.k, nseg, d.off, d.len, d.seed, G);
+        }
     };
     // Load policy per group: a group of one or two lines per lane (small
     // messages) reads with the default policy, longer streams non-temporally.
@@ -925,6 +932,19 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         return contrib;
     };
     auto finish = [&](const Group& C, uint32_t crc) {
+        if (ONE) {
+            // every segment is a whole message ending at E: un-shift the
+            // padding, invert, store
+            uint32_t contrib = C.valid ? crc : 0u;
+            const uint32_t padE = C.valid ? (uint32_t)(C.L0 + ((uint64_t)C.nl << 7) - C.E) : 0u;
+            if (__ballot(padE != 0) != 0 && C.valid) {
+                contrib = gmul(crc, xneg8[padE]);
+            }
+            if (C.valid) {
+                a.out[C.msg] = contrib ^ 0xffffffffu;
+            }
+            return;
+        }
         uint32_t contrib = contribution(C, crc);
         // XOR-reduce each run of adjacent lanes holding the same message, then
         // one store or atomic per run: the run head owns the result.  A
@@ -1580,11 +1600,18 @@ extern "C" int bmqcrc_launch_batch(const BatchArgs* a, void* stream, int num_cus
     if (ev_start) {
         (void)hipEventRecord((hipEvent_t)ev_start, s);
     }
+    const bool one = a->spec == 1u && !a->whole && !(a->tune & 64u);
     if (!(a->tune & 1u)) {  // default: non-temporal LDS-DMA (once-read stream)
-        hipLaunchKernelGGL(k_fold<true>, dim3((unsigned)grid), dim3(kWavesPerBlock * 64), 0, s, *a);
+        if (one) {
+            hipLaunchKernelGGL((k_fold<true, true>), dim3((unsigned)grid),
+                               dim3(kWavesPerBlock * 64), 0, s, *a);
+        } else {
+            hipLaunchKernelGGL((k_fold<true, false>), dim3((unsigned)grid),
+                               dim3(kWavesPerBlock * 64), 0, s, *a);
+        }
     } else {
-        hipLaunchKernelGGL(k_fold<false>, dim3((unsigned)grid), dim3(kWavesPerBlock * 64), 0, s,
-                           *a);
+        hipLaunchKernelGGL((k_fold<false, false>), dim3((unsigned)grid),
+                           dim3(kWavesPerBlock * 64), 0, s, *a);
     }
     if (ev_stop) {
         (void)hipEventRecord((hipEvent_t)ev_stop, s);
