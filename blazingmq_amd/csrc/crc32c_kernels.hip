@@ -50,6 +50,7 @@ typedef __attribute__((address_space(3))) uint8_t lds_u8;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const u32x4 lds_cu4;
+typedef __attribute__((address_space(3))) u32x4 lds_u4;
 
 __constant__ uint32_t c_x2col[31][32] = BMQCRC_X2COL;
 __constant__ uint32_t c_xneg8[136] = BMQCRC_XNEG8;
@@ -806,13 +807,25 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         const uint32_t plo_l = 8u * G.r0 + gS;
         const uint32_t pcnt_l = G.valid ? gE - gS : 0u;
         const uint64_t pb_l = G.L0 - ((uint64_t)G.r0 << 7);
+        // Instruction i reads segments 8i .. 8i+7 (lane l: segment 8i + l/8),
+        // so each lane needs eight other lanes' sources: transposed through a
+        // 1 KiB scratch at the start of slot 0 (free here: no DMA in flight,
+        // and this wave's earlier reads of it complete first, LDS being in
+        // order per wave).  Lane s writes record (s & 7) * 8 + ((s >> 3) ^
+        // (s & 7)); lane l reads records (l >> 3) * 8 + (i ^ (l >> 3)), i =
+        // 0..7 (the XOR spreads one read's eight addresses over the banks).
+        const uint32_t ls = (uint32_t)lane;
+        const uint32_t kq = ls >> 3;
+        *(lds_u4*)(uintptr_t)(wave_lds + 16u * ((ls & 7u) * 8u + (kq ^ (ls & 7u)))) =
+            u32x4{(uint32_t)pb_l, (uint32_t)(pb_l >> 32), plo_l, pcnt_l};
+        __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            const int src = 8 * i + (lane >> 3);
+            const u32x4 v = *(lds_cu4*)(uintptr_t)(wave_lds + 16u * (kq * 8u + ((uint32_t)i ^ kq)));
             const uint32_t pp = ((uint32_t)lane & 7u) ^ ((4u * i + ((uint32_t)lane >> 4)) & 7u);
-            G.pbase[i] = shfl64(pb_l, src) + 16u * pp;
-            G.plo[i] = (uint32_t)__shfl((int)plo_l, src) - pp;
-            G.pcnt[i] = (uint32_t)__shfl((int)pcnt_l, src);
+            G.pbase[i] = (((uint64_t)v.y << 32) | v.x) + 16u * pp;
+            G.plo[i] = v.z - pp;
+            G.pcnt[i] = v.w;
         }
     };
     auto segments = [&](uint32_t len) {
