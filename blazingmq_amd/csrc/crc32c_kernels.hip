@@ -262,37 +262,30 @@ __device__ __forceinline__ uint32_t tab_lookup(uint32_t tab_lds, int k, uint32_t
     return *(const lds_u32*)(uintptr_t)(tab_lds + k * 1024u + b * 4u);
 }
 
-// FIRST: the stream is this one round (zero history), so every tap into the
-// previous round reads zero and is dropped at compile time -- no ring to
-// clear for one-line streams.
-template <bool FIRST>
-__device__ __forceinline__ void tail_rem(const uint32_t (&q)[32], const uint32_t (&p)[32],
-                                         const uint32_t (&m)[32], uint32_t (&R)[32])
+// The last round's taps into the previous round (d + k <= 31): R_d = m_d ^
+// H_d.  A pair (k, k+1) with d + k + 1 <= 31 is p[d + k].
+__device__ __forceinline__ void tail_taps(const uint32_t (&q)[32], const uint32_t (&p)[32],
+                                          uint32_t (&H)[32])
 {
-    // R_d = m_d ^ (taps that stay in the previous round: d + k <= 31); a pair
-    // (k, k+1) with d + k + 1 <= 31 is p[d + k]
 #pragma unroll
     for (int d = 0; d < 32; ++d) {
         uint32_t t[20];
         int nt = 0;
-        t[nt++] = m[d];
-        if (!FIRST) {
 #pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                if (d + kSingles[i] <= 31) {
-                    t[nt++] = q[d + kSingles[i]];
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < 7; ++i) {
-                if (d + kPairs[i] + 1 <= 31) {
-                    t[nt++] = p[d + kPairs[i]];
-                } else if (d + kPairs[i] <= 31) {
-                    t[nt++] = q[d + kPairs[i]];
-                }
+        for (int i = 0; i < 3; ++i) {
+            if (d + kSingles[i] <= 31) {
+                t[nt++] = q[d + kSingles[i]];
             }
         }
-        uint32_t acc = t[0];
+#pragma unroll
+        for (int i = 0; i < 7; ++i) {
+            if (d + kPairs[i] + 1 <= 31) {
+                t[nt++] = p[d + kPairs[i]];
+            } else if (d + kPairs[i] <= 31) {
+                t[nt++] = q[d + kPairs[i]];
+            }
+        }
+        uint32_t acc = nt ? t[0] : 0u;
         int i = 1;
 #pragma unroll
         for (; i + 1 < nt; i += 2) {
@@ -301,7 +294,7 @@ __device__ __forceinline__ void tail_rem(const uint32_t (&q)[32], const uint32_t
         if (i < nt) {
             acc ^= t[i];
         }
-        R[d] = acc;
+        H[d] = acc;
     }
 }
 
@@ -915,13 +908,25 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
             }
         }
         const uint32_t slot = wave_lds + ((R - 1u) & 1u) * kSlotBytes;
+        // R_d = m_d ^ (taps into the previous round): the taps need only the
+        // ring, so they are summed before the last line lands, and the path
+        // from its arrival to the next group's loads is 32 XORs (one-line
+        // streams: no history)
+        uint32_t H[32];
+        if (R == 1) {
+#pragma unroll
+            for (int d = 0; d < 32; ++d) {
+                H[d] = 0u;
+            }
+        } else {
+            tail_taps(q, p, H);
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         uint32_t m[32];
         load_line(R - 1u, slot, m);
-        if (R == 1) {
-            tail_rem<true>(q, p, m, Rm);  // one-line streams: no history
-        } else {
-            tail_rem<false>(q, p, m, Rm);  // every lane's last line: one tail per wave
+#pragma unroll
+        for (int d = 0; d < 32; ++d) {
+            Rm[d] = m[d] ^ H[d];
         }
     };
 
@@ -1074,14 +1079,16 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         // they load while this group's remainder is reduced and combined.
         const Group C = G;
         if (g + stride < ngroups) {
-            const SegDesc d = nxt;
+            // setup first: it reads the descriptors loaded a group ago, and the
+            // compiler's wait for them (which cannot see the DMA waits above)
+            // must not also wait for the loads issued next
+            setup(nxt, g + stride, G);
             const uint32_t s2 = (g + 2u * stride) * 64u + (uint32_t)lane;
             const bool v2 = g + 2u * stride < ngroups && s2 < total;
             nxt = fetch_desc(a, ref2, v2);
             const uint32_t s3 = (g + 3u * stride) * 64u + (uint32_t)lane;
             ref2 = map_segment(a, &pl, s3, g + 3u * stride < ngroups && s3 < total, identity, uni,
                                sorted);
-            setup(d, g + stride, G);
             issue_first_rounds(G);
         }
         finish(C, tail_horner(Rm, tab_lds));
