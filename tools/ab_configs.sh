@@ -3,7 +3,7 @@
 # bench.py run each, on the GPU box.  A variant is "base" (the product
 # build) or a name built by tools/build_variant.sh (variant_<name>.so, e.g.
 # with -DBMQCRC_TUNE_BITS=...); it is swapped in as libbmqcrc.so for its runs.
-#   usage: tools/ab_configs.sh <prefix> "<variants>" [config ...]
+#   usage: [STEPS=K WARMUP=W] tools/ab_configs.sh <prefix> "<variants>" [config ...]
 #   output: gpurun_out/<prefix>.jsonl, one line per (variant, config)
 set -eo pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -21,7 +21,7 @@ for v in $variants; do
     for c in $configs; do
         echo "== variant=$v $c $(date +%T)"
         rc=0
-        timeout -k 10 240 python3 bench.py --config "$c" --steps 20 --warmup 5 \
+        timeout -k 10 240 python3 bench.py --config "$c" --steps ${STEPS:-20} --warmup ${WARMUP:-5} \
             --no-cpu-baseline > "gpurun_out/${prefix}_${v}_$c.log" \
             2> "gpurun_out/${prefix}_${v}_$c.err" || rc=$?
         # 1 = parity mismatches reported by bench.py (diagnostic builds); anything
