@@ -27,6 +27,8 @@ def main():
     runs = [(w, g, 0) for w in (0, 1) for g in (256 * 4, 256 * 8)]
     runs += [(w, g, 0) for w in (2, 3) for g in (256, 512)]
     runs += [(w, g, seg) for w in (4, 5) for g in (256, 512) for seg in (65536, 16384)]
+    if len(sys.argv) > 2 and sys.argv[1] == "--segs":  # k_fold shape, nt, given segment sizes only
+        runs = [(5, g, int(seg)) for seg in sys.argv[2].split(",") for g in (256, 512)]
     for which, grid, seg in runs:
         def launch():
             rc = lib.probe_launch(which, buf.data_ptr(), nbytes, out.data_ptr(), grid, seg,
