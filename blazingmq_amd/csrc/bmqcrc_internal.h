@@ -13,6 +13,7 @@ constexpr int kSlots = 2;                                  // LDS ring depth per
 constexpr int kSlotBytes = kWaveLanes * kLine;             // 8 KiB per round per wave
 constexpr int kLdsBytes = kWavesPerBlock * kSlots * kSlotBytes;  // 64 KiB per block
 constexpr int kTabBytes = 8 * 256 * 4;  // remainder-reduction slicing tables (LDS)
+constexpr int kXbBytes = 4 * 256 * 4;   // move factors x^(8 b 256^i) (LDS)
 constexpr uint32_t kDefaultSegBytes = 16384;
 constexpr int kPlanBlock = 1024;
 constexpr int kPlanMaxBlocks = 256;  // planner grids: contiguous message ranges

@@ -54,6 +54,7 @@ typedef __attribute__((address_space(3))) u32x4 lds_u4;
 
 __constant__ uint32_t c_x2col[31][32] = BMQCRC_X2COL;
 __constant__ uint32_t c_xneg8[136] = BMQCRC_XNEG8;
+__constant__ uint32_t c_xbytes[4][256] = BMQCRC_XBYTES;
 __constant__ uint32_t c_ty[8][256] = BMQCRC_TY;
 
 // All-zero line in device memory: the LDS-DMA source of every 16-byte piece
@@ -122,6 +123,25 @@ __device__ __forceinline__ uint32_t gmul(uint32_t v, uint32_t w)
         w = xand(w >> 1, bitmask(w, 0), 0x82F63B78u);
     }
     return acc;
+}
+
+// v * x^(8 dist) mod P: the move of a CRC past dist zero bytes, as the
+// product of the factors of dist's bytes (tables XBYTES[i][b] = x^(8 b 256^i)
+// in LDS at xb): one lookup per byte position any lane needs and one 160-VALU
+// multiply per factor, against one 64-VALU column pass per exponent bit.
+__device__ __forceinline__ uint32_t mul_xbytes(uint32_t v, uint32_t dist, uint32_t xb)
+{
+    if (__ballot(dist != 0) == 0) {
+        return v;
+    }
+    uint32_t f = *(const lds_u32*)(uintptr_t)(xb + 4u * (dist & 0xffu));
+#pragma unroll
+    for (int i = 1; i < 4; ++i) {
+        if (__ballot((dist >> (8 * i)) != 0) != 0) {
+            f = gmul(f, *(const lds_u32*)(uintptr_t)(xb + 1024u * i + 4u * ((dist >> (8 * i)) & 0xffu)));
+        }
+    }
+    return gmul(v, f);
 }
 
 __device__ __forceinline__ uint32_t mersenne31(uint64_t x)
@@ -667,12 +687,15 @@ __device__ __forceinline__ SegDesc fetch_desc(const BatchArgs& a, SegRef r, bool
 template <bool NT, bool ONE>
 __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kTabBytes + kLdsBytes];
+    // remainder tables, DMA slots, move factors (not needed by ONE: no moves
+    // in its first pass)
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kTabBytes + kLdsBytes + (ONE ? 0 : kXbBytes)];
 
     const int lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t tab_lds = (uint32_t)(uintptr_t)(lds_u8*)lds;
     const uint32_t wave_lds = tab_lds + kTabBytes + wave * (kSlots * kSlotBytes);
+    const uint32_t xb_lds = tab_lds + kTabBytes + kLdsBytes;
 
     // Prologue: every load that depends on nothing is issued before the first
     // wait -- the remainder tables, k_plan's block words and the first group's
@@ -684,6 +707,15 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     for (int i = 0; i < 8; ++i) {
         const uint32_t t = threadIdx.x + (uint32_t)i * (kWavesPerBlock * 64);
         tw[i] = c_ty[t >> 8][t & 255u];
+    }
+    static_assert(4 * 256 == 4 * kWavesPerBlock * 64, "move factors: 4 words per thread");
+    uint32_t xw[4];
+    if (!ONE) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t t = threadIdx.x + (uint32_t)i * (kWavesPerBlock * 64);
+            xw[i] = c_xbytes[t >> 8][t & 255u];
+        }
     }
     const uint32_t whole = ONE ? 0u : a.whole;
     // speculative single launch (no planner ran): every message predicted to
@@ -710,6 +742,13 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     }
     if (threadIdx.x < 136u) {
         xneg8[threadIdx.x] = xn;
+    }
+    if (!ONE) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t t = threadIdx.x + (uint32_t)i * (kWavesPerBlock * 64);
+            *(lds_u32*)(uintptr_t)(xb_lds + 4u * t) = xw[i];
+        }
     }
 
     // BMQCRC_F_WHOLE_MESSAGES and speculative launches: group g = messages
@@ -942,8 +981,11 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         } else if (C.valid) {
             contrib = gmul(crc, xneg8[padE]);
         }
-        const uint32_t e_after = C.valid ? mersenne31(8ull * (C.mend - C.E)) : 0u;
-        contrib = mul_xpow(contrib, e_after);
+        if (ONE) {  // second pass only (mispredicted long messages)
+            contrib = mul_xpow(contrib, C.valid ? mersenne31(8ull * (C.mend - C.E)) : 0u);
+        } else {
+            contrib = mul_xbytes(contrib, C.valid ? (uint32_t)(C.mend - C.E) : 0u, xb_lds);
+        }
         if (C.first) {
             contrib ^= 0xffffffffu;
         }
