@@ -274,3 +274,41 @@ def test_one_line_stop_matches_unshift():
             segment_contrib(arena, S, E, S, mend, first, seed)
         checked += 1
     assert checked > 100
+
+
+def _header_table(name):
+    """A brace-initialised table from the generated crc32c_consts.h."""
+    import os
+    import re
+    p = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "blazingmq_amd",
+                     "csrc", "crc32c_consts.h")
+    text = open(p).read()
+    body = text[text.index("#define %s" % name):]
+    body = body[:body.index("}\n") + 1]
+    return [int(v, 16) for v in re.findall(r"0x([0-9a-f]{8})u", body)]
+
+
+def test_move_byte_tables_match_xpow():
+    """k_fold's move to the message end (mul_xbytes): the product of
+    XBYTES[i][byte i of dist] equals x^(8 dist), for the kernel's own header."""
+    flat = _header_table("BMQCRC_XBYTES")
+    assert len(flat) == 4 * 256
+    xb = [flat[256 * i:256 * (i + 1)] for i in range(4)]
+    rng = np.random.default_rng(11)
+    dists = [0, 1, 255, 256, 65535, 65536, (1 << 24) - 1, 1 << 24, (1 << 32) - 1]
+    dists += [int(d) for d in rng.integers(0, 1 << 32, size=200, dtype=np.uint64)]
+    for dist in dists:
+        f = 1 << 31
+        for i in range(4):
+            f = G.mulmod_r(f, xb[i][(dist >> (8 * i)) & 0xff])
+        assert f == xpow(8 * dist), dist
+    # the move applied to a segment CRC: crc(A || zeros(dist)) = crc(A) * x^(8 dist)
+    a = rng.integers(0, 256, size=64, dtype=np.uint8).tobytes()
+    for dist in (1, 100, 4096, 70000):
+        raw = oracle.crc32c(a + bytes(dist), 0) ^ 0xFFFFFFFF
+        moved = G.mulmod_r(oracle.crc32c(a, 0) ^ 0xFFFFFFFF, 1 << 31)
+        f = 1 << 31
+        for i in range(4):
+            f = G.mulmod_r(f, xb[i][(dist >> (8 * i)) & 0xff])
+        # raw CRCs here include the ~0 initial value, which zeros shift too
+        assert G.mulmod_r(moved, f) == raw
