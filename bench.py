@@ -524,10 +524,10 @@ def main():
         return e2e(args, dev, stream, arena, offs_np, lens_np, total_bytes, world, rank, dist,
                    desc)
 
-    def step(timed):
+    def step(timed, plan=False):
         Crc32c.calculate_batch(arena, offsets, lengths, None, out, seg_bytes=args.seg_bytes,
                                stream=stream, sync=False, time_kernel=timed,
-                               whole_messages=args.whole_messages)
+                               whole_messages=args.whole_messages, plan=plan)
 
     # setup: settle the GPU clocks under this exact load (not part of W or K)
     t_settle = time.perf_counter()
@@ -550,6 +550,21 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
+    launch = bmq.last_launch(local, stream)  # the steady-state step's launch plan
+    # The same K steps with the shape prediction off (BMQCRC_F_PLAN): what a
+    # caller whose batch shapes alternate on one stream pays per batch.
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(False, plan=True)
+    torch.cuda.synchronize(dev)
+    planned = time.perf_counter() - t0
+    planned_launch = bmq.last_launch(local, stream)
+    if world > 1:
+        dist.barrier()
+    step(False)  # back to the predicted shape
     # Second timed pass of the same K steps with HIP events recorded around
     # the dominant kernel (k_fold) on its launch stream: its average duration
     # prices the roofline (events add launch gaps, so `value` comes from the
@@ -563,9 +578,9 @@ def main():
     bytes_all = total_bytes
     kern_max = kern_ms / max(kern_cnt, 1)
     if world > 1:
-        tt = torch.tensor([elapsed, kern_max], dtype=torch.float64)
+        tt = torch.tensor([elapsed, kern_max, planned], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed, kern_max = float(tt[0]), float(tt[1])
+        elapsed, kern_max, planned = float(tt[0]), float(tt[1]), float(tt[2])
         bt = torch.tensor([total_bytes, n], dtype=torch.int64)
         dist.all_reduce(bt)
         bytes_all, n_all = int(bt[0]), int(bt[1])
@@ -626,6 +641,11 @@ def main():
                          "kernel": "k_fold", "kernel_avg_us": round(avg_kern_s * 1e6, 2),
                          "alg_bytes_per_launch": alg_bytes},
             "parity": {"checked_msgs": checked, "mismatches": bad},
+            "kernels_per_step": launch["kernels"],
+            "speculative_segments_per_msg": launch["spec"],
+            "planned_ms_per_step": round(1e3 * planned / args.steps, 4),
+            "planned_value": round(bytes_all / 2**30 * args.steps / planned, 2),
+            "planned_kernels_per_step": planned_launch["kernels"],
         }
         if rehearsal:
             res["rehearsal_single_gpu"] = True
@@ -696,11 +716,11 @@ def strong_scaling(args, bmq, Crc32c, dev, stream, world, rank, dist):
                 bad += int(got[i] != exp)
             del arena, offsets, lengths, out
             torch.cuda.empty_cache()
-        t = torch.tensor([elapsed, bad, total], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        tb = torch.tensor([total], dtype=torch.int64)
-        dist.all_reduce(tb)
-        return float(t[0]), int(t[1]), int(tb[0])
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)       # the slowest rank's window
+        tb = torch.tensor([total, bad], dtype=torch.int64)
+        dist.all_reduce(tb)                            # bytes and mismatches summed
+        return float(t[0]), int(tb[1]), int(tb[0])
 
     lens_r, begin_r = gen(rank, world)
     t_n, bad_n, bytes_n = leg(lens_r, begin_r, True)

@@ -19,6 +19,7 @@ BMQCRC_F_DEVICE_PTRS = 0x1
 BMQCRC_F_ASYNC = 0x2
 BMQCRC_F_TIME_KERNEL = 0x4
 BMQCRC_F_WHOLE_MESSAGES = 0x8
+BMQCRC_F_PLAN = 0x10
 
 
 class BmqCrcError(RuntimeError):
@@ -76,6 +77,11 @@ lib.bmqcrc_fill_synthetic.argtypes = [_vp, _u64, _u64, _u64, ctypes.POINTER(Opts
 lib.bmqcrc_kernel_timing.restype = _int
 lib.bmqcrc_kernel_timing.argtypes = [_int, _vp, ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(_u32)]
+lib.bmqcrc_last_launch.restype = _int
+lib.bmqcrc_last_launch.argtypes = [_int, _vp, ctypes.POINTER(_u32), ctypes.POINTER(_u32),
+                                   ctypes.POINTER(_u32)]
+lib.bmqcrc_forget_shape.restype = _int
+lib.bmqcrc_forget_shape.argtypes = [_int, _vp]
 lib.bmqcrc_host_register.restype = _int
 lib.bmqcrc_host_register.argtypes = [_vp, _u64, _int, ctypes.POINTER(_vp)]
 lib.bmqcrc_host_unregister.restype = _int

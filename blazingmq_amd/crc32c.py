@@ -114,7 +114,7 @@ class Crc32c:
     @staticmethod
     def calculate_batch(arena, offsets, lengths, seeds=None, out=None, *, seg_bytes=0,
                         device=None, stream=None, sync=True, time_kernel=False,
-                        whole_messages=False, devices=None):
+                        whole_messages=False, devices=None, plan=False):
         """Batched CRC32-C of messages ``arena[offsets[i] : offsets[i]+lengths[i]]``.
 
         torch CUDA tensors: ``arena`` uint8, ``offsets`` int64, ``lengths`` /
@@ -124,6 +124,8 @@ class Crc32c:
         ``uint32`` out.  ``whole_messages`` (BMQCRC_F_WHOLE_MESSAGES): one
         lane per message, no planner launches -- for batches of small messages.
         ``devices`` (host arrays only): split the batch over several GPUs.
+        ``plan`` (BMQCRC_F_PLAN, device tensors): run the planner for this
+        batch instead of predicting its shape from the previous batch.
         """
         try:
             import torch
@@ -131,13 +133,13 @@ class Crc32c:
             torch = None
         if torch is not None and isinstance(arena, torch.Tensor) and arena.is_cuda:
             return _batch_torch(torch, arena, offsets, lengths, seeds, out, seg_bytes, stream,
-                                sync, time_kernel, whole_messages)
+                                sync, time_kernel, whole_messages, plan)
         return _batch_host(arena, offsets, lengths, seeds, out, seg_bytes, device,
                            whole_messages, devices)
 
 
 def _batch_torch(torch, arena, offsets, lengths, seeds, out, seg_bytes, stream, sync,
-                 time_kernel=False, whole_messages=False):
+                 time_kernel=False, whole_messages=False, plan=False):
     dev = arena.device
     n = offsets.numel()
     for name, t, dt in (("offsets", offsets, torch.int64), ("lengths", lengths, torch.int32)):
@@ -161,6 +163,8 @@ def _batch_torch(torch, arena, offsets, lengths, seeds, out, seg_bytes, stream, 
         flags |= _native.BMQCRC_F_TIME_KERNEL
     if whole_messages:
         flags |= _native.BMQCRC_F_WHOLE_MESSAGES
+    if plan:
+        flags |= _native.BMQCRC_F_PLAN
     o = _native.make_opts(device=dev.index if dev.index is not None else -1,
                           stream=stream.cuda_stream, flags=flags, seg_bytes=seg_bytes)
     _native.check(_native.lib.bmqcrc_crc32c_batch(
@@ -317,6 +321,23 @@ def kernel_timing(device, stream):
     _native.check(_native.lib.bmqcrc_kernel_timing(device, stream.cuda_stream, ctypes.byref(tot),
                                                   ctypes.byref(cnt)))
     return tot.value, cnt.value
+
+
+def last_launch(device, stream):
+    """Launch plan of the previous batch on (device, stream)
+    (bmqcrc_last_launch): dict(kernels, spec, seg_bytes) -- kernels launched
+    (1 = the fold alone), segments per message a single launch assumed (0 =
+    planned), segment size."""
+    k, u, sb = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+    _native.check(_native.lib.bmqcrc_last_launch(device, stream.cuda_stream, ctypes.byref(k),
+                                                ctypes.byref(u), ctypes.byref(sb)))
+    return {"kernels": k.value, "spec": u.value, "seg_bytes": sb.value}
+
+
+def forget_shape(device, stream):
+    """Drop the batch-shape prediction of (device, stream)
+    (bmqcrc_forget_shape): the next batch there is planned."""
+    _native.check(_native.lib.bmqcrc_forget_shape(device, stream.cuda_stream))
 
 
 def reserve(device, stream, n_msgs, arena_bytes, seg_bytes=0):

@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <map>
 #include <memory>
@@ -115,6 +116,8 @@ struct Workspace {
     // costs speed (k_fold then maps segments by binary search).
     uint32_t* hint_host = nullptr;
     uint32_t* hint_dev = nullptr;
+    // Launch plan of the last batch (bmqcrc_last_launch).
+    uint32_t last_kernels = 0, last_spec = 0, last_seg = 0;
     // Pinned staging ring for gathered host buffers (bmqcrc_crc32c_gather):
     // kGatherSlots chunks of kGatherChunk bytes, each reusable once the event
     // recorded after its H2D copy has completed.
@@ -372,7 +375,7 @@ int run_batch(Ctx& c, uint32_t flags, uint32_t seg, const void* arena, uint64_t 
         a.max_segs = n;
     } else if ((rc = plan_ws(w, n, arena_bytes, seg, &a))) {
         return rc;
-    } else if (!(kTuneBits & 16u)) {
+    } else if (!(kTuneBits & 16u) && !(flags & BMQCRC_F_PLAN)) {
         const uint32_t hint = __atomic_load_n(w->hint_host, __ATOMIC_RELAXED);
         const uint32_t shape = hint & 0xffu, hint_u = hint >> 8;
         if (shape == kHintClosed || shape == kHintIdentity) {
@@ -389,7 +392,7 @@ int run_batch(Ctx& c, uint32_t flags, uint32_t seg, const void* arena, uint64_t 
             a.spec = hint_u;
         }
     }
-    if (!a.whole && host_max_len <= a.seg_bytes) {
+    if (!a.whole && host_max_len <= a.seg_bytes && !(flags & BMQCRC_F_PLAN)) {
         a.spec = 1;  // known, not guessed: every message is one segment
     }
     a.arena = (const uint8_t*)arena;
@@ -416,6 +419,9 @@ int run_batch(Ctx& c, uint32_t flags, uint32_t seg, const void* arena, uint64_t 
         return fail(BMQCRC_EIO, std::string("kernel launch failed: ") +
                                     hipGetErrorString(hipGetLastError()));
     }
+    w->last_spec = a.whole ? 1u : a.spec;
+    w->last_seg = a.seg_bytes;
+    w->last_kernels = n == 0 ? 0u : (a.whole || a.spec) ? 1u : a.map_planned ? 3u : 2u;
     return 0;
 }
 
@@ -479,7 +485,7 @@ int parse_opts(const bmqcrc_opts* opts, bmqcrc_opts* o, uint32_t* seg, int* dev)
     }
     *seg = o->seg_bytes;
     const uint32_t known = BMQCRC_F_DEVICE_PTRS | BMQCRC_F_ASYNC | BMQCRC_F_TIME_KERNEL |
-                           BMQCRC_F_WHOLE_MESSAGES;
+                           BMQCRC_F_WHOLE_MESSAGES | BMQCRC_F_PLAN;
     if (o->flags & ~known) {
         return fail(BMQCRC_EINVAL, "unknown bmqcrc_opts.flags bits");
     }
@@ -501,6 +507,9 @@ int check_ranges(const uint64_t* offsets, const uint32_t* lengths, uint64_t n,
     }
     return 0;
 }
+
+// Device mismatch-index list of a verify: 4 Mi entries (16 MiB) at most.
+constexpr uint64_t kVerifyListCap = 1ull << 22;
 
 int verify_locked(Ctx& c, Workspace* w, const bmqcrc_opts& o, uint32_t seg, bool arena_staged,
                   const void* arena, uint64_t arena_bytes, const uint64_t* offsets,
@@ -663,9 +672,11 @@ int verify_locked(Ctx& c, Workspace* w, const bmqcrc_opts& o, uint32_t seg, bool
 {
     int rc;
     const bool dev_ptrs = (o.flags & BMQCRC_F_DEVICE_PTRS) != 0;
-    // n < 2^32, so every mismatch index fits the device list: exactly
-    // min(n_bad, bad_cap) indices are written.
-    const uint32_t cap = (uint32_t)std::min<uint64_t>(bad_cap, n);
+    // The device list holds at most kVerifyListCap indices (16 MiB), whatever
+    // bad_cap is; a longer answer is taken in windows of that size, so exactly
+    // min(n_bad, bad_cap) indices are still written.
+    const uint64_t want = std::min<uint64_t>(bad_cap, n);
+    const uint32_t cap = (uint32_t)std::min<uint64_t>(want, kVerifyListCap);
     if (n_written) {
         *n_written = 0;
     }
@@ -703,17 +714,26 @@ int verify_locked(Ctx& c, Workspace* w, const bmqcrc_opts& o, uint32_t seg, bool
     HIP_TRY(hipMemcpyAsync(&cnt, w->vcount.p, 4, hipMemcpyDeviceToHost, c.s));
     HIP_TRY(hipStreamSynchronize(c.s));
     *n_bad = cnt;
-    const uint32_t take = std::min(cnt, cap);
-    if (take && cnt > cap) {
-        // more mismatches than slots: the single pass kept an arbitrary
-        // subset, so rebuild the list in index order (lowest `cap` indices)
+    const uint64_t take = std::min<uint64_t>(cnt, want);
+    if (take && cnt <= cap) {
+        // the single pass kept every mismatch: sort the short list
+        std::vector<uint32_t> idx(take);
+        HIP_TRY(hipMemcpyAsync(idx.data(), w->vidx.p, 4ull * take, hipMemcpyDeviceToHost, c.s));
+        HIP_TRY(hipStreamSynchronize(c.s));
+        std::sort(idx.begin(), idx.end());
+        for (uint64_t k = 0; k < take; ++k) {
+            bad_idx[k] = idx[k];
+        }
+    } else if (take) {
+        // more mismatches than device slots: the single pass kept an arbitrary
+        // subset, so rebuild the list in index order, one window at a time
         const uint32_t nb = (uint32_t)std::min<uint64_t>((n + 255) / 256, 4096);
         if ((rc = w->vblock.ensure(4ull * nb))) {
             return rc;
         }
         uint32_t* d_blk = (uint32_t*)w->vblock.p;
         if (bmqcrc_launch_compare_ordered((const uint32_t*)w->out.p, d_exp, n, d_blk, nb,
-                                          nullptr, cap, 0, (void*)c.s)) {
+                                          nullptr, 0, cap, 0, (void*)c.s)) {
             return fail(BMQCRC_EIO, "ordered compare launch failed");
         }
         std::vector<uint32_t> blk(nb);
@@ -726,19 +746,19 @@ int verify_locked(Ctx& c, Workspace* w, const bmqcrc_opts& o, uint32_t seg, bool
             run += k;
         }
         HIP_TRY(hipMemcpyAsync(d_blk, blk.data(), 4ull * nb, hipMemcpyHostToDevice, c.s));
-        if (bmqcrc_launch_compare_ordered((const uint32_t*)w->out.p, d_exp, n, d_blk, nb,
-                                          (uint32_t*)w->vidx.p, cap, 1, (void*)c.s)) {
-            return fail(BMQCRC_EIO, "ordered compare launch failed");
-        }
-        HIP_TRY(hipStreamSynchronize(c.s));  // blk is read by the async H2D copy
-    }
-    if (take) {
-        std::vector<uint32_t> idx(take);
-        HIP_TRY(hipMemcpyAsync(idx.data(), w->vidx.p, 4ull * take, hipMemcpyDeviceToHost, c.s));
-        HIP_TRY(hipStreamSynchronize(c.s));
-        std::sort(idx.begin(), idx.end());
-        for (uint32_t k = 0; k < take; ++k) {
-            bad_idx[k] = idx[k];
+        std::vector<uint32_t> idx(cap);
+        for (uint64_t skip = 0; skip < take; skip += cap) {
+            const uint32_t m = (uint32_t)std::min<uint64_t>(cap, take - skip);
+            if (bmqcrc_launch_compare_ordered((const uint32_t*)w->out.p, d_exp, n, d_blk, nb,
+                                              (uint32_t*)w->vidx.p, (uint32_t)skip, m, 1,
+                                              (void*)c.s)) {
+                return fail(BMQCRC_EIO, "ordered compare launch failed");
+            }
+            HIP_TRY(hipMemcpyAsync(idx.data(), w->vidx.p, 4ull * m, hipMemcpyDeviceToHost, c.s));
+            HIP_TRY(hipStreamSynchronize(c.s));  // also: blk is read by the async H2D copy
+            for (uint32_t k = 0; k < m; ++k) {
+                bad_idx[skip + k] = idx[k];
+            }
         }
     }
     if (n_written) {
@@ -1471,6 +1491,45 @@ int bmqcrc_kernel_timing(int device, void* stream, double* total_ms, uint32_t* c
     return 0;
 }
 
+int bmqcrc_last_launch(int device, void* stream, uint32_t* kernels, uint32_t* spec,
+                       uint32_t* seg_bytes)
+{
+    t_err.clear();
+    DeviceGuard keep_device;
+    int dev, rc;
+    if ((rc = resolve_device(device, &dev))) {
+        return rc;
+    }
+    Workspace* w = workspace(dev, stream);
+    std::lock_guard<std::mutex> g(w->mu);
+    if (kernels) {
+        *kernels = w->last_kernels;
+    }
+    if (spec) {
+        *spec = w->last_spec;
+    }
+    if (seg_bytes) {
+        *seg_bytes = w->last_seg;
+    }
+    return 0;
+}
+
+int bmqcrc_forget_shape(int device, void* stream)
+{
+    t_err.clear();
+    DeviceGuard keep_device;
+    int dev, rc;
+    if ((rc = resolve_device(device, &dev))) {
+        return rc;
+    }
+    Workspace* w = workspace(dev, stream);
+    std::lock_guard<std::mutex> g(w->mu);
+    if (w->hint_host) {
+        __atomic_store_n(w->hint_host, kHintUnknown, __ATOMIC_RELAXED);
+    }
+    return 0;
+}
+
 int bmqcrc_host_register(void* host, uint64_t bytes, int device, void** dev_ptr)
 {
     t_err.clear();
@@ -1518,9 +1577,35 @@ const char* bmqcrc_last_error(void)
     return t_err.c_str();
 }
 
+// Host fallbacks of the C++ spellings (bmqcrc.h).  A fault (EIO) is never
+// silent: the first one in the process is printed with its HIP error.
+static std::atomic<uint64_t> g_fallbacks{0};
+static std::atomic<int32_t> g_fallback_rc{0};
+static std::atomic<bool> g_eio_reported{false};
+
+void bmqcrc_note_host_fallback(int32_t rc)
+{
+    g_fallbacks.fetch_add(1, std::memory_order_relaxed);
+    g_fallback_rc.store(rc, std::memory_order_relaxed);
+    if (rc == BMQCRC_EIO && !g_eio_reported.exchange(true)) {
+        fprintf(stderr,
+                "libbmqcrc: GPU batch failed with BMQCRC_EIO (%s); finishing on the host "
+                "(bmqcrc_host_fallbacks counts every such call)\n",
+                t_err.c_str());
+    }
+}
+
+uint64_t bmqcrc_host_fallbacks(int32_t* last_rc)
+{
+    if (last_rc) {
+        *last_rc = g_fallback_rc.load(std::memory_order_relaxed);
+    }
+    return g_fallbacks.load(std::memory_order_relaxed);
+}
+
 uint32_t bmqcrc_version(void)
 {
-    return (2u << 16) | 1u;
+    return (2u << 16) | 2u;
 }
 
 }  // extern "C"

@@ -87,12 +87,12 @@ extern "C" __attribute__((visibility("hidden"))) int bmqcrc_launch_blob_combine(
 extern "C" __attribute__((visibility("hidden"))) int bmqcrc_launch_fill(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t begin,
                                   void* stream);
 // Ordered mismatch list: pass 0 writes per-block counts to block_cnt, pass 1
-// reads the exclusive prefix from block_cnt and writes the bad_cap lowest
-// mismatching indices to bad_idx (ascending).
+// reads the exclusive prefix from block_cnt and writes the mismatching indices
+// of ranks [skip, skip + bad_cap) in index order to bad_idx (ascending).
 extern "C" __attribute__((visibility("hidden"))) int bmqcrc_launch_compare_ordered(const uint32_t* got, const uint32_t* expected,
                                             uint64_t n, uint32_t* block_cnt, uint32_t nblocks,
-                                            uint32_t* bad_idx, uint32_t bad_cap, int pass,
-                                            void* stream);
+                                            uint32_t* bad_idx, uint32_t skip, uint32_t bad_cap,
+                                            int pass, void* stream);
 // Host-buffer verify with the descriptor walk overlapped (bmqcrc_host.cpp):
 // `prepare` runs on the calling thread while the arena is copied to the device
 // on a helper thread; it returns 0 and the (offset, length, expected CRC)

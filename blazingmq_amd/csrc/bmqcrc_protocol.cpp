@@ -427,8 +427,15 @@ int walk_recovery(const uint8_t* j, uint64_t jlen, const uint8_t* d, uint64_t dl
             }
         } else if (h.type == kRecQueueOp) {  // :1717-2233
             const uint64_t qkey = key5(rec + 22), akey = key5(rec + 27);
-            if ((int32_t)be32(rec + 32) != kOpPurge || before_queue_deletion(qkey, pos) ||
-                !live(qkey)) {
+            const int32_t op = (int32_t)be32(rec + 32);
+            if (before_queue_deletion(qkey, pos)) {
+                continue;  // :1778-1787, :2003-2013
+            }
+            if (op == kOpAddition && !qv->with_csl && !live(qkey)) {
+                // an ADDITION whose CREATION the first pass did not see (:2018-2030)
+                return fail_at(BMQCRC_RECOVERY_INVALID_QUEUE_KEY, pos);
+            }
+            if (op != kOpPurge || !live(qkey)) {
                 continue;  // only a whole-queue purge of a live queue skips messages
             }
             if (akey == 0) {

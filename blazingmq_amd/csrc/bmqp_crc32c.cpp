@@ -13,9 +13,15 @@ namespace {
 // reference's interface has no error channel (bmqp_crc32c.h:240-243), so the
 // batch overloads then finish on the host, bit-exact, with the library's own
 // SSE4.2 CRC.  Argument errors (BMQCRC_EINVAL) are returned as they are.
+// Every fallback is recorded (bmqcrc_host_fallbacks); a fault (EIO) is also
+// reported on stderr once.
 bool gpuFailure(int rc)
 {
-    return rc == BMQCRC_ENODEV || rc == BMQCRC_ENOMEM || rc == BMQCRC_EIO;
+    if (rc == BMQCRC_ENODEV || rc == BMQCRC_ENOMEM || rc == BMQCRC_EIO) {
+        bmqcrc_note_host_fallback(rc);
+        return true;
+    }
+    return false;
 }
 
 }  // close unnamed namespace

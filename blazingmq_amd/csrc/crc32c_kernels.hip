@@ -1531,9 +1531,11 @@ __global__ void k_compare_count(const uint32_t* got, const uint32_t* expected, u
     }
 }
 
+// Ranks [skip, skip + bad_cap) of the ordered list go to bad_idx[rank - skip]
+// (the host takes a long list in windows of a fixed device buffer).
 __global__ void k_compare_emit(const uint32_t* got, const uint32_t* expected, uint64_t n,
                                uint64_t chunk, const uint32_t* block_off, uint32_t* bad_idx,
-                               uint32_t bad_cap)
+                               uint32_t skip, uint32_t bad_cap)
 {
     __shared__ uint32_t wave_cnt[16];
     const uint64_t lo = (uint64_t)blockIdx.x * chunk;
@@ -1541,7 +1543,8 @@ __global__ void k_compare_emit(const uint32_t* got, const uint32_t* expected, ui
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t nwaves = blockDim.x >> 6;
     uint32_t run = block_off[blockIdx.x];
-    for (uint64_t base = lo; base < hi && run < bad_cap; base += blockDim.x) {
+    const uint64_t end = (uint64_t)skip + bad_cap;
+    for (uint64_t base = lo; base < hi && run < end; base += blockDim.x) {
         const uint64_t i = base + threadIdx.x;
         const bool bad = i < hi && got[i] != expected[i];
         const uint64_t m = __ballot(bad);
@@ -1555,8 +1558,9 @@ __global__ void k_compare_emit(const uint32_t* got, const uint32_t* expected, ui
             before += (w < wave) ? wave_cnt[w] : 0u;
             total += wave_cnt[w];
         }
-        if (bad && before + below < bad_cap) {
-            bad_idx[before + below] = (uint32_t)i;
+        const uint64_t rank = (uint64_t)before + below;
+        if (bad && rank >= skip && rank < end) {
+            bad_idx[rank - skip] = (uint32_t)i;
         }
         run += total;
         __syncthreads();
@@ -1696,8 +1700,8 @@ extern "C" int bmqcrc_launch_compare(const uint32_t* got, const uint32_t* expect
 
 extern "C" int bmqcrc_launch_compare_ordered(const uint32_t* got, const uint32_t* expected,
                                             uint64_t n, uint32_t* block_cnt, uint32_t nblocks,
-                                            uint32_t* bad_idx, uint32_t bad_cap, int pass,
-                                            void* stream)
+                                            uint32_t* bad_idx, uint32_t skip, uint32_t bad_cap,
+                                            int pass, void* stream)
 {
     if (n == 0 || nblocks == 0) {
         return 0;
@@ -1708,7 +1712,7 @@ extern "C" int bmqcrc_launch_compare_ordered(const uint32_t* got, const uint32_t
                            got, expected, n, chunk, block_cnt);
     } else {
         hipLaunchKernelGGL(k_compare_emit, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, got,
-                           expected, n, chunk, block_cnt, bad_idx, bad_cap);
+                           expected, n, chunk, block_cnt, bad_idx, skip, bad_cap);
     }
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }

@@ -238,14 +238,23 @@ def recovery_selection_py(journal, data, with_csl=False, queue_keys=()):
                 return fail(RC_INVALID_SYNC_PT_SUB_TYPE, pos)
             if doff == 0 or d.size < doff:
                 return fail(RC_INVALID_DATA_OFFSET, pos)
-            if sp_lease == 0 or sp_lease > lease:
+            # the reference's order (:1647-1713): lease 0, seq 0, lease ahead, seq mismatch
+            if sp_lease == 0:
                 return fail(RC_INVALID_PRIMARY_LEASE_ID, pos)
-            if sp_seq == 0 or (sp_lease == lease and sp_seq != seq):
+            if sp_seq == 0:
+                return fail(RC_INVALID_SEQ_NUMBER, pos)
+            if sp_lease > lease:
+                return fail(RC_INVALID_PRIMARY_LEASE_ID, pos)
+            if sp_lease == lease and sp_seq != seq:
                 return fail(RC_INVALID_SEQ_NUMBER, pos)
         elif t == REC_QUEUE_OP:
-            qkey, akey = bytes(r[22:27]), bytes(r[27:32])
-            if _int(r, 32, 4) == OP_PURGE and not before_deletion(qkey, pos) and qkey in live \
-                    and akey == NULL_KEY:
+            qkey, akey, op = bytes(r[22:27]), bytes(r[27:32]), _int(r, 32, 4)
+            if before_deletion(qkey, pos):
+                continue
+            if op == OP_ADDITION and not with_csl and qkey not in live:
+                # an ADDITION whose CREATION the first pass did not see (:2018-2030)
+                return fail(RC_INVALID_QUEUE_KEY, pos)
+            if op == OP_PURGE and qkey in live and akey == NULL_KEY:
                 purged.add(qkey)
         elif t == REC_DELETION:
             qkey, guid = bytes(r[23:28]), bytes(r[28:44])

@@ -55,6 +55,11 @@ extern "C" {
  * journal records): correct for any lengths, but a long message keeps its
  * whole wave busy for its full length. */
 #define BMQCRC_F_WHOLE_MESSAGES 0x8u
+/* ABI 2.2.  Plan this batch (planner launches before the fold) instead of
+ * launching it on the guess that it has the previous batch's shape on the same
+ * (device, stream); see bmqcrc_last_launch.  What a caller whose batch shapes
+ * alternate pays per batch. */
+#define BMQCRC_F_PLAN 0x10u
 
 typedef struct bmqcrc_opts {
     uint32_t struct_size; /* sizeof(bmqcrc_opts) */
@@ -165,6 +170,20 @@ int bmqcrc_fill_synthetic(void* dev_dst, uint64_t nbytes, uint64_t seed, uint64_
  * since the previous query; waits for those events, then resets. */
 int bmqcrc_kernel_timing(int device, void* stream, double* total_ms, uint32_t* count);
 
+/* ABI 2.2.  Launch plan of the previous batch CRC'd on (device, stream):
+ * *kernels = kernels it launched (1: the fold alone; 2: planner + fold; 3:
+ * planner, size-class sort, fold), *spec = the segments per message its single
+ * launch assumed (0: planned; 1 also for BMQCRC_F_WHOLE_MESSAGES), *seg_bytes =
+ * the segment size used.  Any pointer may be NULL. */
+int bmqcrc_last_launch(int device, void* stream, uint32_t* kernels, uint32_t* spec,
+                       uint32_t* seg_bytes);
+
+/* ABI 2.2.  Drop the batch-shape prediction of (device, stream): the next
+ * batch there is planned (k_plan runs) instead of being launched on the guess
+ * that it has the previous batch's shape.  For callers that know their next
+ * batch differs; a batch still in flight may set the prediction again. */
+int bmqcrc_forget_shape(int device, void* stream);
+
 /* Zero-copy input: page-lock `bytes` of ordinary host memory at `host` and map
  * it into the GPU address space (hipHostRegister, mapped + portable).
  * *dev_ptr receives the device-side address of `host`; pass it as the arena
@@ -179,6 +198,18 @@ int bmqcrc_device_count(void);
 
 /* Message for the last failing call on this thread ("" if none). */
 const char* bmqcrc_last_error(void);
+
+/* ABI 2.2.  The C++ spellings at the reference's call sites
+ * (bmqp::Crc32c::calculateBatch, the bmqcrc_protocol.h wrappers) finish on the
+ * host when a batch call fails with BMQCRC_ENODEV, ENOMEM or EIO, because the
+ * reference's interface has no error channel.  Each such fallback is recorded
+ * here: bmqcrc_host_fallbacks returns how many happened in this process and
+ * stores the last failing code in *last_rc (may be NULL).  The first EIO (a
+ * kernel fault or a sticky HIP error, as opposed to a missing device) is also
+ * printed once on stderr with its HIP error, so a broken GPU context is never
+ * hidden behind correct host results. */
+void bmqcrc_note_host_fallback(int32_t rc);
+uint64_t bmqcrc_host_fallbacks(int32_t* last_rc);
 
 /* ABI version: (major << 16) | minor. */
 uint32_t bmqcrc_version(void);

@@ -166,12 +166,18 @@ int bmqcrc_csl_validate(const void* log, uint64_t len, const uint8_t* expected_l
  * fails for want of a GPU (BMQCRC_ENODEV, ENOMEM, EIO) they redo the same
  * walk and CRC every message on the host with the library's own SSE4.2 code
  * (bmqcrc_crc32c), bit-exact.  Format errors (BMQCRC_EINVAL) are returned.
- * The C-ABI batch entry points above stay GPU-only. */
+ * Every fallback is recorded (bmqcrc_host_fallbacks, bmqcrc.h); a fault (EIO)
+ * is also reported on stderr once.  The C-ABI batch entry points above stay
+ * GPU-only. */
 namespace BloombergLP {
 namespace bmqcrc_detail {
 inline bool gpuFailure(int64_t rc)
 {
-    return rc == BMQCRC_ENODEV || rc == BMQCRC_ENOMEM || rc == BMQCRC_EIO;
+    if (rc == BMQCRC_ENODEV || rc == BMQCRC_ENOMEM || rc == BMQCRC_EIO) {
+        bmqcrc_note_host_fallback((int32_t)rc);
+        return true;
+    }
+    return false;
 }
 inline uint32_t be32(const uint8_t* p)
 {

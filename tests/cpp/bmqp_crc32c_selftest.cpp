@@ -501,6 +501,15 @@ int main(int argc, char** argv)
     if (have_fixture) {
         recovery_verify(journal, data);
     }
+    // every host fallback is recorded: none with a GPU, one per spelling without
+    int32_t last_rc = 0;
+    const uint64_t fallbacks = bmqcrc_host_fallbacks(&last_rc);
+    if (bmqcrc_device_count() > 0) {
+        CHECK_EQ((unsigned)fallbacks, 0u);
+    } else {
+        CHECK_EQ((unsigned)(fallbacks > 0), 1u);
+        CHECK_EQ((unsigned)last_rc, (unsigned)BMQCRC_ENODEV);
+    }
     printf("%s: %d failure(s)\n", g_fail ? "FAIL" : "PASS", g_fail);
     return g_fail ? 1 : 0;
 }

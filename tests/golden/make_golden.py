@@ -15,6 +15,16 @@ Sources (all in /root/reference, read as text):
       and test.bmq_journal (copied verbatim) with the journal CRC printed by
       bmqstoragetool in detail_result.txt:15,53 (3381945770) for the two
       MESSAGE records at DATA offsets 40 and 64 (payload_dump.txt).
+  * src/applications/bmqstoragetool/integration-tests/data/test.bmq_csl (copied
+      verbatim): a broker-written cluster state ledger, with what
+      bmqstoragetool prints for it -- detail_csl_result.txt (SNAPSHOT@388,
+      COMMIT@540, LogId 87EDF15DC0, sequence numbers, header and advisory
+      words), short_csl_result.txt, summary_csl_result.txt (the one queue and
+      its key 26DACDC974) and test_cslfile.py's searches (a COMMIT at offset
+      316 with seqnum 1-4, none at 317; two SNAPSHOTs from the beginning; one
+      UPDATE and one COMMIT strictly between offsets 88 and 388).
+  * queueop_result.txt / summary_queueop_journalop_result.txt: the journal's
+      QueueOp CREATION at offset 104 for that key, and its record counts.
   * RFC 3720 section B.4 (iSCSI CRC32C test patterns) as external known answers.
 """
 import json
@@ -135,10 +145,88 @@ def main():
         "records": [{"record_offset": 40, "header_bytes": 12, "app_data_len": 11, "crc": crcs[0]},
                     {"record_offset": 64, "header_bytes": 12, "app_data_len": 11, "crc": crcs[1]}],
     }
+    out["csl"] = csl_fixture()
+    out["journal_queue_ops"] = queue_op_fixture()
+    assert out["csl"]["queue_key"] == out["journal_queue_ops"]["creation"]["queue_key"]
     with open(os.path.join(HERE, "crc32c_vectors.json"), "w") as f:
         json.dump(out, f, indent=1)
     print("wrote crc32c_vectors.json:", {k: len(v) if isinstance(v, list) else 1
                                          for k, v in out.items()})
+
+
+CSL_TYPES = {"SNAPSHOT": 1, "UPDATE": 2, "COMMIT": 3, "ACK": 4}
+
+
+def csl_fixture():
+    """The ledger and bmqstoragetool's view of it (ClusterStateRecordType,
+    mqbc_clusterstateledgerprotocol.h:154)."""
+    shutil.copyfile(os.path.join(DATA_DIR, "test.bmq_csl"), os.path.join(HERE, "test.bmq_csl"))
+    detail = open(os.path.join(DATA_DIR, "detail_csl_result.txt")).read()
+    recs = []
+    for blk in detail.split("RecordType           : ")[1:]:
+        def field(name):
+            return re.search(name + r"\s*:\s*(\S+)", blk).group(1)
+        recs.append({"offset": int(field("Offset")), "type": CSL_TYPES[blk.split()[0]],
+                     "log_id": field("LogId"), "elector_term": int(field("ElectorTerm")),
+                     "sequence_number": int(field("SequenceNumber")),
+                     "header_words": int(field("HeaderWords")),
+                     "advisory_words": int(field("LeaderAdvisoryWords")),
+                     "epoch": int(field("Epoch"))})
+    assert [(r["offset"], r["type"]) for r in recs] == [(388, 1), (540, 3)], recs
+    short = open(os.path.join(DATA_DIR, "short_csl_result.txt")).read()
+    short_offs = [int(x) for x in re.findall(r"offset = (\d+)", short)]
+    assert short_offs == [r["offset"] for r in recs], short_offs
+    assert set(re.findall(r"logId = (\w+)", short)) == {recs[0]["log_id"]}
+    summary = open(os.path.join(DATA_DIR, "summary_csl_result.txt")).read()
+    keys = re.findall(r"key = \[ (\w+) \]", summary)
+    assert len(keys) == 1, keys
+    tests_py = open(os.path.join(DATA_DIR, "..", "test_cslfile.py")).read()
+
+    def const(name):
+        return re.search(name + r'\s*=\s*"?([^"\n]+)"?', tests_py).group(1)
+    seq1 = [int(x) for x in const("TEST_SEARCH_SEQNUM_1").split("-")]
+    # test_search_offset: --offset=316 finds 1 commit record, --offset=317 none;
+    # test_search_seqnum: --seqnum=1-4 finds 1 commit record;
+    # test_short_result --csl-from-begin: "2 snapshot record";
+    # test_search_range: offsets in (88, 388) hold 1 update and 1 commit, no snapshot
+    assert 'b"1 commit record"' in tests_py and 'b"2 snapshot record"' in tests_py
+    return {
+        "file": "test.bmq_csl", "log_id": recs[0]["log_id"], "records": recs,
+        "queue_key": keys[0],
+        "search": {
+            "commit_at": {"offset": int(const("TEST_SEARCH_OFFSET_1")),
+                          "elector_term": seq1[0], "sequence_number": seq1[1]},
+            "not_a_record": int(const("TEST_SEARCH_OFFSET_2")),
+            "snapshots_from_begin": 2,
+            "between": {"gt": int(const("TEST_OFFSET_LOWER")),
+                        "lt": int(const("TEST_OFFSET_UPPER")),
+                        "counts": {"1": 0, "2": 1, "3": 1, "4": 0}},
+        },
+    }
+
+
+def queue_op_fixture():
+    """The journal's QueueOp and JournalOp records as bmqstoragetool lists them."""
+    qop = open(os.path.join(DATA_DIR, "queueop_result.txt")).read()
+
+    def field(name):
+        return re.search(name + r"\s*:\s*(\S+)", qop).group(1)
+    summ = open(os.path.join(DATA_DIR, "summary_queueop_journalop_result.txt")).read()
+
+    def count(label):
+        return int(re.search(label + r"\s*:?\s*(\d+)", summ).group(1))
+    out = {
+        "creation": {"offset": int(field("Offset")), "queue_key": field("QueueKey"),
+                     "app_key": field("AppKey"), "op": field("QueueOpType"),
+                     "primary_lease_id": int(field("PrimaryLeaseId")),
+                     "sequence_number": int(field("SequenceNumber")),
+                     "qlist_offset_words": int(field("QLIST OffsetWords"))},
+        "queue_op_records": count("Total number of queueOp records"),
+        "creation_ops": count("Number of 'creation' operations"),
+        "journal_op_records": count("Number of journalOp records"),
+    }
+    assert out["creation"]["offset"] == 104 and out["creation"]["op"] == "CREATION", out
+    return out
 
 
 if __name__ == "__main__":

@@ -110,13 +110,62 @@ def test_put_event_deferred_equals_immediate(cuda):
     assert (n, n_bad, bad.tolist()) == (len(apps), len(victims), victims)
 
 
+def _oracle_record(advisory, **kw):
+    """A ledger record whose CRC comes from the oracle, not from the product's
+    scalar path (csl.append_record's default)."""
+    body = csl.append_record(advisory, crc=0, **kw)[:-4]
+    return body + oracle.crc32c(body).to_bytes(4, "big")
+
+
 def _csl_log(n, rng, key=b"\x01\x02\x03\x04\x05"):
-    recs = [csl.append_record(rng.integers(0, 256, size=int(rng.integers(1, 3000)),
-                                           dtype=np.uint8).tobytes(),
-                              record_type=int(rng.integers(1, 5)), elector_term=3,
-                              sequence_number=i + 1, timestamp=123567 + i)
+    recs = [_oracle_record(rng.integers(0, 256, size=int(rng.integers(1, 3000)),
+                                        dtype=np.uint8).tobytes(),
+                           record_type=int(rng.integers(1, 5)), elector_term=3,
+                           sequence_number=i + 1, timestamp=123567 + i)
             for i in range(n)]
     return csl.file_header(key) + b"".join(recs), recs
+
+
+def _fixture_ledger(golden):
+    with open(os.path.join(GOLD, golden["csl"]["file"]), "rb") as f:
+        return f.read(), bytes.fromhex(golden["csl"]["log_id"])
+
+
+def test_csl_validate_reference_ledger(cuda, golden):
+    """bmqstoragetool's broker-written ledger (test.bmq_csl, LogId 87EDF15DC0):
+    the batched validateLog accepts it to its last byte; a flipped advisory
+    byte in the SNAPSHOT at 388 (detail_csl_result.txt) or the COMMIT at 540
+    is INVALID_CHECKSUM at that record; a wrong log id is INVALID_LOG_ID."""
+    log, log_id = _fixture_ledger(golden)
+    assert csl.validate_log(log, log_id) == (csl.SUCCESS, len(log), None) == \
+        (csl.SUCCESS, 612, None)
+    for rec in golden["csl"]["records"]:
+        b = bytearray(log)
+        b[rec["offset"] + 4 * rec["header_words"] + 5] ^= 0x20
+        assert csl.validate_log(bytes(b), log_id) == (csl.INVALID_CHECKSUM, 0, rec["offset"])
+    b = bytearray(log)
+    b[540 + 4 * 18 - 1] ^= 0x01  # the COMMIT's stored CRC itself
+    assert csl.validate_log(bytes(b), log_id) == (csl.INVALID_CHECKSUM, 0, 540)
+    assert csl.validate_log(log, b"\x87\xed\xf1\x5d\xc1")[0] == csl.INVALID_LOG_ID
+
+
+def test_csl_mode_recovery_of_reference_partition(cuda, golden):
+    """The journal/DATA fixture recovered with the cluster state the ledger
+    names (summary_csl_result.txt: key 26DACDC974): the outstanding message at
+    644 is CRC'd and verifies; a cluster state without that key fails the
+    CREATION at 104 (queueop_result.txt) with INVALID_QUEUE_KEY."""
+    j = np.fromfile(os.path.join(GOLD, "test.bmq_journal"), np.uint8)
+    d = np.fromfile(os.path.join(GOLD, "test.bmq_data"), np.uint8)
+    key = bytes.fromhex(golden["csl"]["queue_key"])
+    res = storage.verify_partition(j, d, with_csl=True, queue_keys=[key])
+    assert (res["recovery_rc"], res["n_messages"], res["n_bad"]) == (0, 1, 0)
+    d2 = d.copy()
+    d2[76 + 3] ^= 1
+    res = storage.verify_partition(j, d2, with_csl=True, queue_keys=[key])
+    assert res["n_bad"] == 1 and res["bad_record_offsets"].tolist() == [644]
+    res = storage.verify_partition(j, d, with_csl=True, queue_keys=[b"\x01\x02\x03\x04\x05"])
+    assert (res["recovery_rc"], res["error_record_offset"]) == \
+        (storage.RC_INVALID_QUEUE_KEY, golden["journal_queue_ops"]["creation"]["offset"])
 
 
 def test_csl_validate_log(cuda):
@@ -131,6 +180,7 @@ def test_csl_validate_log(cuda):
     assert rc == csl.REACHED_END_OF_LOG
     # test5: a record with an incorrect CRC
     wrong = csl.append_record(b"advisory", csl.UPDATE, 3, 8, 123567, crc=111111)
+    assert oracle.crc32c(wrong[:-4]) != 111111
     assert csl.validate_log(log + wrong, key) == (csl.INVALID_CHECKSUM, 0, len(log))
     # a cleanly invalid record header ends the walk with success
     zeros = bytes(64)

@@ -268,6 +268,46 @@ def _oracle_all(arena_t, offs, lens):
     return oracle.batch(host, offs.astype(np.uint64), lens, nthreads=16)
 
 
+def test_config_1k_x_4KiB_planned_then_speculative(cuda):
+    """configs[0] exactly as bench.py runs it (1,000 x 4,096 B of synthetic
+    stream 0xB1A2E5, contiguous, automatic segments): the first batch on a
+    fresh stream is planned; the next ones are ONE k_fold launch that assumes
+    u = 16 segments of 256 B per message (BatchArgs::spec).  Every CRC of
+    every batch equals the oracle's (the reference's CPU case for this size
+    is bmqp_crc32c.h:122)."""
+    import torch
+    from blazingmq_amd import fill_synthetic, forget_shape, last_launch
+    n, size, seed = 1000, 4096, 0xB1A2E5
+    arena = torch.empty(n * size, dtype=torch.uint8, device=cuda)
+    s = torch.cuda.Stream(cuda)
+    with torch.cuda.stream(s):
+        fill_synthetic(arena, seed, stream=s)
+    s.synchronize()
+    host = oracle.fill_payload(0, n * size, seed)
+    assert np.array_equal(arena.cpu().numpy(), host)
+    offs = np.arange(n, dtype=np.int64) * size
+    lens = np.full(n, size, dtype=np.uint32)
+    exp = oracle.batch(host, offs.astype(np.uint64), lens)
+    o = torch.from_numpy(offs).to(cuda)
+    ln = torch.from_numpy(lens.view(np.int32)).to(cuda)
+
+    def run():
+        got = Crc32c.calculate_batch(arena, o, ln, stream=s)
+        s.synchronize()
+        bad = np.nonzero(got.cpu().numpy().view(np.uint32) != exp)[0]
+        assert bad.size == 0, bad[:8]
+        return last_launch(cuda.index, s)
+
+    forget_shape(cuda.index, s)
+    planned = run()
+    assert planned["spec"] == 0 and planned["kernels"] >= 2 and planned["seg_bytes"] == 256
+    for _ in range(3):
+        assert run() == {"kernels": 1, "spec": 16, "seg_bytes": 256}
+    forget_shape(cuda.index, s)
+    assert run()["spec"] == 0                   # planned again, then speculative again
+    assert run()["spec"] == 16
+
+
 def test_config_1M_x_256B_full(cuda):
     arena, offs, lens, got = _device_batch_from_stream(cuda, np.full(1 << 20, 256), 1)
     assert np.array_equal(got, _oracle_all(arena, offs, lens))
@@ -526,6 +566,25 @@ def test_host_batch_and_verify_over_device_listings(cuda, devices):
     assert n_bad == len(victims) and bad.tolist() == victims
     n_bad, bad = Crc32c.verify_batch(arena, offs, lens, wrong, bad_cap=5, devices=devices)
     assert n_bad == len(victims) and bad.tolist() == victims[:5]
+
+
+def test_verify_list_longer_than_device_buffer(cuda):
+    """The device keeps at most 4 Mi mismatch indices whatever bad_cap is; a
+    longer answer comes back in windows: every index, ascending, exactly
+    min(n_bad, bad_cap) of them."""
+    n = (1 << 22) + 300_001
+    arena = np.arange(256, dtype=np.uint8)
+    offs = (np.arange(n, dtype=np.uint64) * 7) % 200
+    lens = (np.arange(n, dtype=np.uint32) % 50)
+    exp = oracle.batch(arena, offs, lens, nthreads=8)
+    wrong = exp ^ 1
+    wrong[::3] = exp[::3]                        # a third of them intact
+    bad_all = np.nonzero(wrong != exp)[0]
+    n_bad, bad = Crc32c.verify_batch(arena, offs, lens, wrong, bad_cap=n)
+    assert n_bad == bad_all.size and np.array_equal(bad, bad_all)
+    cap = (1 << 22) + 17
+    n_bad, bad = Crc32c.verify_batch(arena, offs, lens, wrong, bad_cap=cap)
+    assert n_bad == bad_all.size and np.array_equal(bad, bad_all[:cap])
 
 
 def test_speculative_uniform_launch(cuda):

@@ -316,6 +316,69 @@ def test_csl_mode_rejects_deleting_a_live_queue():
     assert r["recovery_rc"] == 0 and r["record_offset"].size == 0
 
 
+def test_addition_without_creation_fails_recovery():
+    """Without CSL an ADDITION whose queue has no CREATION seen by the first
+    pass fails recovery with rc_INVALID_QUEUE_KEY (mqbs_filestore.cpp:
+    2018-2030); the messages met above it (backwards) were already CRC'd."""
+    w = S.PartitionWriter()
+    w.queue_op(S.OP_CREATION, Q1)
+    w.message(b"below the bad record", Q1)
+    bad = w.queue_op(S.OP_ADDITION, Q2)          # Q2 was never created
+    above, _ = w.message(b"above it", Q1)
+    j, d = w.files()
+    r = _same(j, d)
+    assert (r["recovery_rc"], r["error_record_offset"]) == (S.RC_INVALID_QUEUE_KEY, bad)
+    assert r["record_offset"].tolist() == [above]
+    # with CSL naming Q2 the ADDITION is fine (the reference checks it in the first pass)
+    r = _same(j, d, with_csl=True, queue_keys=[Q1, Q2])
+    assert r["recovery_rc"] == 0 and r["record_offset"].size == 2
+
+
+def test_addition_after_queue_deletion_fails_recovery():
+    """An ADDITION after its queue's DELETION with no re-creation names a dead
+    queue; an ADDITION before the DELETION is ignored (:2003-2013)."""
+    w = S.PartitionWriter()
+    w.queue_op(S.OP_CREATION, Q1)
+    w.queue_op(S.OP_ADDITION, Q1)                # before the deletion: ignored
+    w.message(b"deleted with its queue", Q1)
+    w.queue_op(S.OP_DELETION, Q1)
+    j0, d0 = w.files()
+    r = _same(j0, d0)
+    assert r["recovery_rc"] == 0 and r["record_offset"].size == 0
+    bad = w.queue_op(S.OP_ADDITION, Q1)          # after it: the queue is dead
+    j, d = w.files()
+    r = _same(j, d)
+    assert (r["recovery_rc"], r["error_record_offset"]) == (S.RC_INVALID_QUEUE_KEY, bad)
+    # an ADDITION of a re-created queue is fine
+    w.queue_op(S.OP_CREATION, Q2)
+    w.queue_op(S.OP_ADDITION, Q2)
+    j, d = w.files()
+    r = _same(j, d)
+    assert (r["recovery_rc"], r["error_record_offset"]) == (S.RC_INVALID_QUEUE_KEY, bad)
+
+
+@pytest.mark.parametrize("sp_lease,sp_seq,rc", [
+    (0, 0, S.RC_INVALID_PRIMARY_LEASE_ID),       # lease 0 is checked first
+    (9, 0, S.RC_INVALID_SEQ_NUMBER),             # then seq 0, before 'lease ahead'
+    (9, 5, S.RC_INVALID_PRIMARY_LEASE_ID),
+    (1, 999, S.RC_INVALID_SEQ_NUMBER),
+])
+def test_sync_point_checks_in_reference_order(sp_lease, sp_seq, rc):
+    """SyncPt checks run in the reference's order (mqbs_filestore.cpp:
+    1647-1713): lease 0, seq 0, lease above the current one, seq mismatch."""
+    w = S.PartitionWriter(lease_id=1)
+    w.queue_op(S.OP_CREATION, Q1)
+    sp = w.sync_point()
+    above, _ = w.message(b"after the sync point", Q1)
+    j, d = w.files()
+    j = j.copy()
+    j[sp + 28:sp + 36] = np.frombuffer(sp_seq.to_bytes(8, "big"), np.uint8)
+    j[sp + 40:sp + 44] = np.frombuffer(sp_lease.to_bytes(4, "big"), np.uint8)
+    r = _same(j, d)
+    assert (r["recovery_rc"], r["error_record_offset"]) == (rc, sp)
+    assert r["record_offset"].tolist() == [above]
+
+
 def test_empty_journal():
     w = S.PartitionWriter()
     j, d = w.files()
