@@ -681,7 +681,7 @@ def strong_scaling(args, bmq, Crc32c, dev, stream, world, rank, dist):
         if n > 1:
             np.cumsum(lens_np[:-1], dtype=np.int64, out=offs_np[1:])
         total = int(lens_np.sum(dtype=np.uint64))
-        elapsed, bad = 0.0, 0
+        elapsed, bad, checked = 0.0, 0, 0
         if active:
             arena = torch.empty(max(total, 8), dtype=torch.uint8, device=dev)
             _fill_slice(bmq, arena, seed, begin)
@@ -714,18 +714,19 @@ def strong_scaling(args, bmq, Crc32c, dev, stream, world, rank, dist):
                 exp = oracle.crc32c(oracle.fill_payload(begin + int(offs_np[i]), int(lens_np[i]),
                                                         seed), 0, "hw")
                 bad += int(got[i] != exp)
+                checked += 1
             del arena, offsets, lengths, out
             torch.cuda.empty_cache()
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)       # the slowest rank's window
-        tb = torch.tensor([total, bad], dtype=torch.int64)
+        tb = torch.tensor([total, bad, checked], dtype=torch.int64)
         dist.all_reduce(tb)                            # bytes and mismatches summed
-        return float(t[0]), int(tb[1]), int(tb[0])
+        return float(t[0]), int(tb[1]), int(tb[0]), int(tb[2])
 
     lens_r, begin_r = gen(rank, world)
-    t_n, bad_n, bytes_n = leg(lens_r, begin_r, True)
+    t_n, bad_n, bytes_n, chk_n = leg(lens_r, begin_r, True)
     lens_1, begin_1 = gen(0, 1) if rank == 0 else (np.zeros(1, np.uint32), 0)
-    t_1, bad_1, _ = leg(lens_1, begin_1, rank == 0)
+    t_1, bad_1, _, chk_1 = leg(lens_1, begin_1, rank == 0)
     gib = bytes_n / 2**30 * args.steps
     return {"config": "zipf_4M: " + CONFIGS["zipf_4M"][0], "scaling": "strong",
             "value": round(gib / t_n, 2), "unit": "GiB/s", "n_gpus": world,
@@ -734,6 +735,7 @@ def strong_scaling(args, bmq, Crc32c, dev, stream, world, rank, dist):
             "one_gpu_ms_per_step": round(1e3 * t_1 / args.steps, 4),
             "speedup": round(t_1 / t_n, 3), "payload_bytes_total": bytes_n,
             "one_gpu_leg": "the whole batch on rank 0's GPU in the same run",
+            "parity": {"checked_msgs": chk_n + chk_1, "mismatches": bad_n + bad_1},
             "_bad": bad_n + bad_1}
 
 
