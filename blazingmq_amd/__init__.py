@@ -6,8 +6,8 @@ The product is the C-ABI library ``lib/libbmqcrc.so`` (HIP kernels for gfx950
 """
 from .crc32c import (Blob, BmqCrcError, Crc32c, HostRegistration,  # noqa: F401
                      calculate_batch_multi, calculate_batch_ptr, device_count, fill_synthetic,
-                     forget_shape, kernel_timing, last_launch, reserve)
+                     forget_shape, kernel_timing, last_launch, plan_wait, reserve)
 
 __all__ = ["Blob", "BmqCrcError", "Crc32c", "HostRegistration", "calculate_batch_multi",
-           "calculate_batch_ptr", "device_count", "fill_synthetic", "forget_shape",
+           "calculate_batch_ptr", "device_count", "fill_synthetic", "forget_shape", "plan_wait",
            "kernel_timing", "last_launch", "reserve"]

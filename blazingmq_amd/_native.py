@@ -82,6 +82,9 @@ lib.bmqcrc_last_launch.argtypes = [_int, _vp, ctypes.POINTER(_u32), ctypes.POINT
                                    ctypes.POINTER(_u32)]
 lib.bmqcrc_forget_shape.restype = _int
 lib.bmqcrc_forget_shape.argtypes = [_int, _vp]
+if hasattr(lib, "bmqcrc_plan_wait"):  # ABI 2.3 (an older build loads for same-box A/B)
+    lib.bmqcrc_plan_wait.restype = _int
+    lib.bmqcrc_plan_wait.argtypes = [_int, _vp, _u64, ctypes.POINTER(_u64)]
 lib.bmqcrc_host_register.restype = _int
 lib.bmqcrc_host_register.argtypes = [_vp, _u64, _int, ctypes.POINTER(_vp)]
 lib.bmqcrc_host_unregister.restype = _int

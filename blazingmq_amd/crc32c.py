@@ -340,6 +340,17 @@ def forget_shape(device, stream):
     _native.check(_native.lib.bmqcrc_forget_shape(device, stream.cuda_stream))
 
 
+def plan_wait(device, stream, wait_us=1000):
+    """Longest wait (microseconds) of the single-pass planner's blocks for
+    each other on (device, stream) before a ragged batch's size-class map is
+    given up (bmqcrc_plan_wait; results stay exact, the fold then searches).
+    Returns how many planned batches there gave up their map so far."""
+    n = ctypes.c_uint64()
+    _native.check(_native.lib.bmqcrc_plan_wait(device, stream.cuda_stream, int(wait_us),
+                                              ctypes.byref(n)))
+    return n.value
+
+
 def reserve(device, stream, n_msgs, arena_bytes, seg_bytes=0):
     """Pre-size the workspace of (device, stream) for batches of up to n_msgs
     messages over arena_bytes (bmqcrc_reserve): afterwards a device-pointer

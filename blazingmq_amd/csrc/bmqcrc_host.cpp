@@ -103,7 +103,10 @@ struct DevBuf {
 // Planner + staging scratch for one (device, stream).
 struct Workspace {
     std::mutex mu;
-    DevBuf seg_first, block_sum, seginfo, bhist;
+    DevBuf seg_first, block_sum, seginfo, bhist, plan_sync;
+    uint32_t plan_epoch = 0;  // k_plan_map launches on this workspace (BatchArgs::plan_epoch)
+    uint64_t map_wait_ticks = 100000;  // 1 ms (bmqcrc_plan_wait)
+
     // host-pointer staging
     DevBuf arena, offsets, lengths, seeds, out;
     // verify / blobs
@@ -224,7 +227,8 @@ static void split_ranges(uint64_t items, uint64_t* per, uint32_t* blocks)
     *blocks = (uint32_t)((tiles + tiles_per - 1) / tiles_per);
 }
 
-int plan_ws(Workspace* w, uint64_t n, uint64_t arena_bytes, uint32_t seg, BatchArgs* a)
+int plan_ws(Workspace* w, hipStream_t s, uint64_t n, uint64_t arena_bytes, uint32_t seg,
+            BatchArgs* a)
 {
     const uint64_t max_segs = max_segs_for(n, arena_bytes, seg);
     split_ranges(n, &a->per_msg, &a->nblocks);
@@ -232,9 +236,20 @@ int plan_ws(Workspace* w, uint64_t n, uint64_t arena_bytes, uint32_t seg, BatchA
     if ((rc = w->seg_first.ensure(4 * std::max<uint64_t>(n, 1))) ||
         (rc = w->block_sum.ensure(12ull * kPlanMaxBlocks)) ||
         (rc = w->seginfo.ensure(8 * max_segs)) ||
-        (rc = w->bhist.ensure(4ull * kBuckets * kPlanMaxBlocks))) {
+        (rc = w->bhist.ensure(4ull * kBuckets * kPlanMaxBlocks)) ||
+        (rc = w->plan_sync.ensure(8ull * (kSyncFlags + kPlanMaxBlocks)))) {
         return rc;
     }
+    if (w->plan_sync.fresh) {  // zero counters, no given-up epoch (stream-ordered)
+        HIP_TRY(hipMemsetAsync(w->plan_sync.p, 0, w->plan_sync.bytes, s));
+    }
+    w->plan_epoch = w->plan_epoch + 1u;
+    if (w->plan_epoch == 0) {
+        w->plan_epoch = 1;
+    }
+    a->plan_sync = (unsigned long long*)w->plan_sync.p;
+    a->plan_epoch = w->plan_epoch;
+    a->map_wait_ticks = w->map_wait_ticks;
     if (!w->hint_host) {
         void* h = nullptr;
         HIP_TRY(hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocPortable |
@@ -373,7 +388,7 @@ int run_batch(Ctx& c, uint32_t flags, uint32_t seg, const void* arena, uint64_t 
     if (flags & BMQCRC_F_WHOLE_MESSAGES) {
         a.whole = 1;  // identity map over messages: no planner workspace
         a.max_segs = n;
-    } else if ((rc = plan_ws(w, n, arena_bytes, seg, &a))) {
+    } else if ((rc = plan_ws(w, c.s, n, arena_bytes, seg, &a))) {
         return rc;
     } else if (!(kTuneBits & 16u) && !(flags & BMQCRC_F_PLAN)) {
         const uint32_t hint = __atomic_load_n(w->hint_host, __ATOMIC_RELAXED);
@@ -1430,7 +1445,7 @@ int bmqcrc_reserve(int device, void* stream, uint64_t n_msgs, uint64_t arena_byt
     BatchArgs a;
     uint32_t per_cu;
     auto_shape(n_msgs, arena_bytes, st->num_cus, &seg_bytes, &per_cu);  // as the batch call will
-    return plan_ws(w, n_msgs, arena_bytes, seg_bytes, &a);
+    return plan_ws(w, (hipStream_t)stream, n_msgs, arena_bytes, seg_bytes, &a);
 }
 
 int bmqcrc_fill_synthetic(void* dev_dst, uint64_t nbytes, uint64_t seed, uint64_t begin,
@@ -1530,6 +1545,30 @@ int bmqcrc_forget_shape(int device, void* stream)
     return 0;
 }
 
+int bmqcrc_plan_wait(int device, void* stream, uint64_t wait_us, uint64_t* voided)
+{
+    t_err.clear();
+    DeviceGuard keep_device;
+    int dev, rc;
+    DeviceState* st = nullptr;
+    if ((rc = resolve_device(device, &dev)) || (rc = device_state(dev, &st))) {
+        return rc;
+    }
+    HIP_TRY(hipSetDevice(dev));
+    Workspace* w = workspace(dev, stream);
+    std::lock_guard<std::mutex> g(w->mu);
+    w->map_wait_ticks = wait_us > (UINT64_MAX / 100) ? UINT64_MAX : wait_us * 100;
+    if (voided) {
+        // k_plan_map counts its launches that gave up their map (plan_sync[3])
+        unsigned long long n = 0;
+        if (w->plan_sync.p) {
+            HIP_TRY(hipMemcpy(&n, (const uint8_t*)w->plan_sync.p + 24, 8, hipMemcpyDeviceToHost));
+        }
+        *voided = n;
+    }
+    return 0;
+}
+
 int bmqcrc_host_register(void* host, uint64_t bytes, int device, void** dev_ptr)
 {
     t_err.clear();
@@ -1605,7 +1644,7 @@ uint64_t bmqcrc_host_fallbacks(int32_t* last_rc)
 
 uint32_t bmqcrc_version(void)
 {
-    return (2u << 16) | 2u;
+    return (2u << 16) | 3u;
 }
 
 }  // extern "C"

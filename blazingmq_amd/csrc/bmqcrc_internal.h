@@ -17,6 +17,7 @@ constexpr int kXbBytes = 4 * 256 * 4;   // move factors x^(8 b 256^i) (LDS)
 constexpr uint32_t kDefaultSegBytes = 16384;
 constexpr int kPlanBlock = 1024;
 constexpr int kPlanMaxBlocks = 256;  // planner grids: contiguous message ranges
+constexpr int kSyncFlags = 16;       // BatchArgs::plan_sync: first arrival flag
 
 constexpr int kBuckets = 16;            // segment size classes: floor(log2(lines))
 
@@ -24,12 +25,33 @@ constexpr int kBuckets = 16;            // segment size classes: floor(log2(line
 // -DBMQCRC_TUNE_BITS=...); the product is built with 0.  bit0 disables the
 // non-temporal LDS-DMA loads, bit1 forces a 1-block/CU k_fold grid, bit3
 // forces 2, bit4 always builds the size-class map (no shape prediction),
-// bit5 reads one- and two-line groups non-temporally too.
+// bit5 reads one- and two-line groups non-temporally too, bit7 plans ragged
+// batches with the round-2 pair k_plan<true> + k_plan_sort instead of the
+// single-pass k_plan_map.
 #ifndef BMQCRC_TUNE_BITS
 #define BMQCRC_TUNE_BITS 0u
 #endif
 constexpr uint32_t kTuneBits = BMQCRC_TUNE_BITS;
 constexpr bool kShortDefaultPolicy = (kTuneBits & 32u) == 0;
+// bit8 turns off the remainder-step skip of one-line groups (A/B).
+constexpr bool kHornerSkip = (kTuneBits & 256u) == 0;
+// Streams right-aligned at piece granularity when that saves a line or the
+// stream is at most this many lines; longer streams otherwise keep a 128-byte
+// aligned start, whose lines are whole cache lines (right-aligning every
+// stream cost Zipf's k_fold 2.3 %, one line 0.5 %: profiles/r03/ab/ab3_*).
+#ifndef BMQCRC_RIGHT_ALIGN_LINES
+#define BMQCRC_RIGHT_ALIGN_LINES 1u
+#endif
+constexpr uint32_t kRightAlignLines = BMQCRC_RIGHT_ALIGN_LINES;
+#ifndef BMQCRC_RIGHT_ALIGN
+#define BMQCRC_RIGHT_ALIGN 1
+#endif
+constexpr bool kRightAlign = BMQCRC_RIGHT_ALIGN != 0;  // 0: round 2's 128-byte aligned streams
+// The ONE kernel's remainder step as two independent chains (A/B knob).
+#ifndef BMQCRC_SPLIT_HORNER
+#define BMQCRC_SPLIT_HORNER 0
+#endif
+constexpr bool kSplitHorner = BMQCRC_SPLIT_HORNER != 0;
 
 struct BatchArgs {
     const uint8_t* arena;      // device
@@ -66,6 +88,13 @@ struct BatchArgs {
     // segments at a time -- correct for any batch, only slower when the
     // guess was wrong.
     uint32_t spec;
+    // Single-pass planner (k_plan_map): [2] the epoch of a launch whose map
+    // was given up (k_fold then ignores seginfo), [3] how many launches gave
+    // theirs up, [kSyncFlags + b] block b's arrival flag (the epoch of the
+    // launch it last arrived in).  Zeroed once when allocated.
+    unsigned long long* plan_sync;
+    uint32_t plan_epoch;       // k_plan_map launch tag on this workspace, never 0
+    uint64_t map_wait_ticks;   // k_plan_map's grid-wide wait limit (100 MHz wall clock)
 };
 
 constexpr uint32_t kHintUnknown = 0;

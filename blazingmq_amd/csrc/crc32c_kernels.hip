@@ -56,6 +56,7 @@ __constant__ uint32_t c_x2col[31][32] = BMQCRC_X2COL;
 __constant__ uint32_t c_xneg8[136] = BMQCRC_XNEG8;
 __constant__ uint32_t c_xbytes[4][256] = BMQCRC_XBYTES;
 __constant__ uint32_t c_ty[8][256] = BMQCRC_TY;
+__constant__ uint32_t c_ty16[4][256] = BMQCRC_TY16;
 
 // All-zero line in device memory: the LDS-DMA source of every 16-byte piece
 // that lies outside a segment's bytes, and of every round outside its stream.
@@ -318,11 +319,17 @@ __device__ __forceinline__ void tail_taps(const uint32_t (&q)[32], const uint32_
     }
 }
 
+// SKIP: R[0 .. 2 SKIP) is zero in every lane of the wave, so the first SKIP
+// steps would leave c = 0 and are not compiled in (one-line groups, whose
+// remainder is the line itself: right-aligned messages of at most 64 bytes
+// leave 16 leading zero words).  A compile-time count: per-step uniform
+// branches cost 2-4 % on two-line groups (profiles/r03/ab/ab2_*.jsonl).
+template <int SKIP = 0>
 __device__ __forceinline__ uint32_t tail_horner(const uint32_t (&R)[32], uint32_t tab_lds)
 {
     uint32_t c = 0;
 #pragma unroll
-    for (int d = 0; d < 32; d += 2) {
+    for (int d = 2 * SKIP; d < 32; d += 2) {
         const uint32_t v = c ^ R[d];
         const uint32_t w = R[d + 1];
         const uint32_t hi = xor3(tab_lookup(tab_lds, 4, v & 0xffu),
@@ -334,6 +341,43 @@ __device__ __forceinline__ uint32_t tail_horner(const uint32_t (&R)[32], uint32_
         c = xor3(hi, lo, tab_lookup(tab_lds, 7, v >> 24) ^ tab_lookup(tab_lds, 3, w >> 24));
     }
     return c;
+}
+
+// Two independent chains (round 3, kSplitHorner): words 0..15 and 16..31 are
+// reduced side by side, c_a = sum_{d<16} R_d y^(16-d) and c_b = sum_{d>=16}
+// R_d y^(32-d), then raw = c_a * y^16 + c_b (four lookups in TY16 tables,
+// LDS at t16_lds).  Eight dependent steps instead of sixteen.
+__device__ __forceinline__ uint32_t horner_step(uint32_t c, uint32_t r0, uint32_t r1,
+                                                uint32_t tab_lds)
+{
+    const uint32_t v = c ^ r0;
+    const uint32_t hi = xor3(tab_lookup(tab_lds, 4, v & 0xffu),
+                             tab_lookup(tab_lds, 5, (v >> 8) & 0xffu),
+                             tab_lookup(tab_lds, 6, (v >> 16) & 0xffu));
+    const uint32_t lo = xor3(tab_lookup(tab_lds, 0, r1 & 0xffu),
+                             tab_lookup(tab_lds, 1, (r1 >> 8) & 0xffu),
+                             tab_lookup(tab_lds, 2, (r1 >> 16) & 0xffu));
+    return xor3(hi, lo, tab_lookup(tab_lds, 7, v >> 24) ^ tab_lookup(tab_lds, 3, r1 >> 24));
+}
+
+template <int SKIP>
+__device__ __forceinline__ uint32_t tail_horner2(const uint32_t (&R)[32], uint32_t tab_lds,
+                                                 uint32_t t16_lds)
+{
+    static_assert(SKIP == 0 || SKIP == 8, "two chains: all words, or the second half");
+    uint32_t ca = 0, cb = 0;
+#pragma unroll
+    for (int d = 0; d < 16; d += 2) {
+        if (SKIP == 0) {
+            ca = horner_step(ca, R[d], R[d + 1], tab_lds);
+        }
+        cb = horner_step(cb, R[16 + d], R[17 + d], tab_lds);
+    }
+    if (SKIP == 8) {
+        return cb;
+    }
+    return cb ^ xor3(tab_lookup(t16_lds, 0, ca & 0xffu), tab_lookup(t16_lds, 1, (ca >> 8) & 0xffu),
+                     tab_lookup(t16_lds, 2, (ca >> 16) & 0xffu) ^ tab_lookup(t16_lds, 3, ca >> 24));
 }
 
 // Word w (0..31) of this lane's 128-byte line in an LDS slot (the pieces are
@@ -617,8 +661,9 @@ __device__ __forceinline__ PlanTotals plan_totals(const BatchArgs& a, PlanLds* p
 }
 
 // Geometry of segment k of a message [mstart, mstart+len): byte range
-// [S, E) (internal boundaries 128-byte aligned), first line L0, lines of the
-// folded stream (covering the seed word of the first segment) and of data.
+// [S, E) (internal boundaries 128-byte aligned), the stream's start L0 (16-byte
+// aligned, see below), lines of the folded stream (covering the seed word of
+// the first segment) and of data.
 struct SegGeom {
     uint64_t S, E, L0;
     uint32_t nl, nl_data;
@@ -631,9 +676,28 @@ __device__ __forceinline__ SegGeom seg_geom(uint64_t mstart, uint32_t len, uint3
     const uint64_t mend = mstart + len;
     g.S = (k == 0) ? mstart : ((mstart + (uint64_t)k * SEG) & ~127ull);
     g.E = (k + 1 == nseg) ? mend : ((mstart + (uint64_t)(k + 1) * SEG) & ~127ull);
-    g.L0 = g.S & ~127ull;
     const uint64_t need_end = (k == 0 && g.E < g.S + 4) ? g.S + 4 : g.E;
-    g.nl = (uint32_t)((need_end - g.L0 + 127u) >> 7);
+    // Right-aligned at piece granularity (round 3): the stream ends with the
+    // 16-byte piece holding its last byte and starts nl lines before, nl the
+    // fewest lines that hold pieces [S/16, that piece].  The stream is a run
+    // of 16-byte pieces of memory, not of 128-byte lines (pieces outside
+    // [S, E) come from the zero line anyway), so a message that straddles a
+    // line boundary but fits 128 bytes is one round, not two, and the zero
+    // padding after E -- undone by one 160-VALU multiply per lane whenever a
+    // lane of the wave has any -- is under 16 bytes, none when E is 16-byte
+    // aligned.  Applied when it saves a line or the stream is one line
+    // (kRightAlignLines); longer streams keep whole-cache-line rounds.
+    const uint64_t pe = (need_end + 15u) & ~15ull;
+    const uint32_t nl_r = (uint32_t)((pe - (g.S & ~15ull) + 127u) >> 7);
+    const uint64_t L0_l = g.S & ~127ull;
+    const uint32_t nl_l = (uint32_t)((need_end - L0_l + 127u) >> 7);
+    if (kRightAlign && (nl_r < nl_l || nl_r <= kRightAlignLines)) {
+        g.nl = nl_r;
+        g.L0 = pe - ((uint64_t)nl_r << 7);
+    } else {
+        g.nl = nl_l;
+        g.L0 = L0_l;
+    }
     g.nl_data = (uint32_t)((g.E - g.L0 + 127u) >> 7);
     return g;
 }
@@ -689,7 +753,10 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
 {
     // remainder tables, DMA slots, move factors (not needed by ONE: no moves
     // in its first pass)
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kTabBytes + kLdsBytes + (ONE ? 0 : kXbBytes)];
+    // (the ONE kernel keeps the y^16 tables of the two-chain remainder step
+    // where the others keep the move factors)
+    __shared__ __attribute__((aligned(16))) uint8_t
+        lds[kTabBytes + kLdsBytes + ((ONE && !kSplitHorner) ? 0 : kXbBytes)];
 
     const int lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -710,11 +777,11 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     }
     static_assert(4 * 256 == 4 * kWavesPerBlock * 64, "move factors: 4 words per thread");
     uint32_t xw[4];
-    if (!ONE) {
+    if (!ONE || kSplitHorner) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const uint32_t t = threadIdx.x + (uint32_t)i * (kWavesPerBlock * 64);
-            xw[i] = c_xbytes[t >> 8][t & 255u];
+            xw[i] = ONE ? c_ty16[t >> 8][t & 255u] : c_xbytes[t >> 8][t & 255u];
         }
     }
     const uint32_t whole = ONE ? 0u : a.whole;
@@ -723,8 +790,12 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     const uint32_t spec_mode = ONE ? 1u : a.spec;
     const uint32_t spec_u = spec_mode ? spec_mode : 1u;
     PlanWords pw = {0u, 0u, 0u, 0u};
+    uint32_t map_void = 0u;  // k_plan_map gave up its map for this launch
     if (!whole && !spec_mode) {
         pw = plan_load(a);
+        if (a.map_planned && a.plan_sync) {
+            map_void = (uint32_t)a.plan_sync[2] == a.plan_epoch;
+        }
     }
     // x^(-8p) un-shift table -> LDS too: a per-lane index, so from constant
     // memory it would be a vector load with a full memory latency per group
@@ -743,7 +814,7 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     if (threadIdx.x < 136u) {
         xneg8[threadIdx.x] = xn;
     }
-    if (!ONE) {
+    if (!ONE || kSplitHorner) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const uint32_t t = threadIdx.x + (uint32_t)i * (kWavesPerBlock * 64);
@@ -774,7 +845,7 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     // the size-class order exists only if the histogram and k_plan_sort ran
     // (and seginfo could hold every segment)
     const uint32_t sorted =
-        (wholef || !a.map_planned || identity || uni || total > a.max_segs) ? 0u : 1u;
+        (wholef || !a.map_planned || identity || uni || total > a.max_segs || map_void) ? 0u : 1u;
     const uint32_t ngroups = (total + 63u) / 64u;
     const uint32_t SEG = a.seg_bytes;
     const uint64_t arena = (uint64_t)(uintptr_t)a.arena;
@@ -803,7 +874,7 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         uint64_t pbase[8];
         uint32_t plo[8], pcnt[8];
         uint64_t E, L0, mend;
-        uint32_t msg, k, nseg, nl, R, r0, sl, jE, eE, c0;
+        uint32_t msg, k, nseg, nl, R, r0, sl, jE, eE, c0, hskip;
         bool valid, first, lo_part, hi_part;
     };
     // Geometry of one lane's segment k of a message of nseg segments.
@@ -823,6 +894,15 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         // every lane invalid (a speculative group of queued messages): one
         // round of zeros, nothing stored
         G.R = max(wave_max(G.nl), 1u);
+        // one-line group: the remainder is the line; its leading zero word
+        // pairs (before the lowest S of the wave) need no remainder step
+        G.hskip = 0u;
+        if (kHornerSkip && G.R == 1u) {
+            // every lane's S in the line's second half (one ballot: this sits
+            // before the next group's loads)
+            const uint32_t sl0 = G.valid ? (uint32_t)(geo.S - geo.L0) : 128u;
+            G.hskip = __ballot(sl0 < 64u) == 0 ? 8u : 0u;
+        }
         // right-aligned stream: this lane's line j is round r0 + j
         G.r0 = G.R - G.nl;
         G.sl = G.valid ? (uint32_t)(geo.S - G.L0) : 0u;  // S's offset in line 0
@@ -1133,7 +1213,12 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
                                sorted);
             issue_first_rounds(G);
         }
-        finish(C, tail_horner(Rm, tab_lds));
+        if (ONE && kSplitHorner) {
+            finish(C, C.hskip ? tail_horner2<8>(Rm, tab_lds, xb_lds)
+                              : tail_horner2<0>(Rm, tab_lds, xb_lds));
+        } else {
+            finish(C, C.hskip ? tail_horner<8>(Rm, tab_lds) : tail_horner(Rm, tab_lds));
+        }
     }
     if (spec_mode && long_seen) {
         second_pass();
@@ -1494,6 +1579,500 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_sort(BatchArgs a)
     }
 }
 
+// ------------------------------------------------ single-pass planner
+// k_plan_map (ragged batches, round 3): one launch does what k_plan<true>
+// and k_plan_sort did in two.  Phase 1 (every block, its contiguous message
+// range): segment counts, the size-class histogram and the block-local
+// prefix, kept in registers; the block words and the histogram are published.
+// The blocks then meet once, grid-wide; after that every block reads all
+// histograms and writes the rest: (message, k) of its segments into its
+// slice of every class -- exactly k_plan_sort's global class-major order --
+// plus seg_first and the out[] initialisation, which phase 1 defers so that
+// the arrival's L2 write-back carries only the block words.  (A block-major
+// order -- each block's slice sorted by class, offsets by a decoupled
+// look-back, no grid-wide wait -- was measured first: k_fold's grid-stride
+// waves then draw a binomial mix of 16-round and 1-round groups, and Zipf's
+// k_fold ran 7 % slower, profiles/r03/ab/ab1_*.jsonl.)
+//
+// Safety of the wait: a grid of <= kPlanMaxBlocks blocks normally fits the
+// GPU at once, but nothing guarantees it (other streams, other processes).
+// A block that has waited map_wait_ticks (1 ms by default, bmqcrc_plan_wait)
+// without seeing every arrival marks the map invalid for this launch
+// (plan_sync[2] = epoch, plan_sync[3] counts such launches), writes its
+// seg_first and leaves; k_fold then ignores seginfo and maps segments by
+// binary search over seg_first.  Arrival flags carry the launch's epoch, so
+// nothing needs resetting between launches.
+#ifndef BMQCRC_MAP_REG_TILES
+#define BMQCRC_MAP_REG_TILES 4
+#endif
+constexpr uint32_t kMapRegTiles = BMQCRC_MAP_REG_TILES;  // tiles kept in registers across the wait
+#ifndef BMQCRC_PLAN_DIAG
+#define BMQCRC_PLAN_DIAG 0  // timing diagnostics only (see below); the product is built with 0
+#endif
+
+#if BMQCRC_PLAN_DIAG >= 3
+// diagnostic build only: per-block wall-clock stamps of the last launch
+// (start, phase 1 done, wait done, end), read by bmqcrc_diag_plan_trace
+__device__ unsigned long long g_plan_trace[kPlanMaxBlocks][4];
+#define PLAN_STAMP(k)                                                        \
+    if (threadIdx.x == 0) {                                                  \
+        g_plan_trace[blockIdx.x][k] = wall_clock64();                        \
+    }
+#else
+#define PLAN_STAMP(k)
+#endif
+
+__global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
+{
+    PLAN_STAMP(0)
+    __shared__ uint32_t wsum[40];
+    __shared__ uint32_t sh[4];
+    __shared__ uint32_t hist[kBuckets];
+    __shared__ uint32_t run[kBuckets];
+    __shared__ uint32_t part[2][kPlanBlock / kBuckets][kBuckets];
+    __shared__ unsigned long long segs64;
+    __shared__ uint32_t go;
+    const uint32_t nb = a.nblocks, ep = a.plan_epoch, bid = blockIdx.x;
+    unsigned long long* const sync = a.plan_sync;
+    if (threadIdx.x == 0) {
+        sh[1] = 0;            // messages with != 1 segment
+        sh[2] = 0xffffffffu;  // min segments per message
+        sh[3] = 0;            // max segments per message
+        segs64 = 0;
+    }
+    if (threadIdx.x < kBuckets) {
+        hist[threadIdx.x] = 0;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    constexpr uint64_t kTile = (uint64_t)kPlanBlock * kPlanV;
+    const uint64_t lo = (uint64_t)bid * a.per_msg;
+    const uint64_t hi = min(lo + a.per_msg, a.n);
+    const uint32_t ntiles = hi > lo ? (uint32_t)((hi - lo + kTile - 1) / kTile) : 0u;
+    const uint32_t seg = a.seg_bytes;
+    const uint32_t seg_shift = (seg & (seg - 1u)) == 0 ? (uint32_t)__builtin_ctz(seg) : 0u;
+    const uint32_t c_full = size_class(seg >> 7);
+    const bool one_tile = ntiles <= 1u;
+    auto segments = [&](uint32_t len) {
+        return len ? (seg_shift ? ((len - 1u) >> seg_shift) : (len - 1u) / seg) + 1u : 0u;
+    };
+
+    // Thread t of tile [base, base + kTile) owns messages base + 4t .. base + 4t + 3.
+    auto load = [&](uint64_t base, uint32_t (&L)[kPlanV], uint64_t (&O)[kPlanV]) {
+#pragma unroll
+        for (uint32_t v = 0; v < kPlanV; ++v) {
+            const uint64_t i = base + (uint64_t)threadIdx.x * kPlanV + v;
+            L[v] = i < hi ? a.lengths[i] : 0u;
+            O[v] = i < hi ? a.offsets[i] : 0ull;
+        }
+    };
+    // seg_first (the block-local prefix from run0) and out[] for one tile
+    auto tile_words = [&](uint64_t base, const uint32_t (&L)[kPlanV], uint32_t run0,
+                          bool write_sf) {
+        uint32_t r = run0;
+#pragma unroll
+        for (uint32_t v = 0; v < kPlanV; ++v) {
+            const uint64_t i = base + (uint64_t)threadIdx.x * kPlanV + v;
+            const uint32_t ns = segments(L[v]);
+            if (i < hi) {
+                if (write_sf) {
+                    a.seg_first[i] = r;
+                }
+                if (ns != 1u) {  // XOR-accumulated in k_fold (from 0; empty: the seed)
+                    a.out[i] = L[v] ? 0u : (a.seeds ? a.seeds[i] : 0u);
+                }
+            }
+            r += ns;
+        }
+    };
+    // Phase 1, per tile (the next tile's loads in flight meanwhile).  The
+    // first kMapRegTiles tiles keep their lengths, classes and prefix in
+    // registers and defer their writes; later tiles write as k_plan does.
+    uint32_t Lr[kMapRegTiles][kPlanV], Cr[kMapRegTiles], R0[kMapRegTiles];
+    uint32_t full = 0, carry = 0, mn = 0xffffffffu, mx = 0, non1 = 0;
+    uint64_t mine64 = 0;
+    uint32_t nxt[kPlanV];
+    uint64_t nxo[kPlanV];
+    if (ntiles) {
+        load(lo, nxt, nxo);
+    }
+    // (all register tiles loaded up front measured slower: 18.7 -> 22.8 us
+    // for phase 1 on Zipf, profiles/r03/ab/planner_phase_stamps.jsonl)
+    auto count_tile = [&](uint32_t t, uint32_t (&L)[kPlanV], uint32_t& cls, uint32_t& run0,
+                          bool defer) {
+        const uint64_t base = lo + (uint64_t)t * kTile;
+        uint64_t O[kPlanV];
+#pragma unroll
+        for (uint32_t v = 0; v < kPlanV; ++v) {
+            L[v] = nxt[v];
+            O[v] = nxo[v];
+        }
+        if (t + 1u < ntiles) {
+            load(base + kTile, nxt, nxo);  // the next tile in flight during this one
+        }
+        cls = 0;
+        uint32_t sum = 0;
+#pragma unroll
+        for (uint32_t v = 0; v < kPlanV; ++v) {
+            uint32_t c;
+            const uint32_t ns = msg_segments(a, O[v], L[v], seg_shift, &c);
+            full += ns ? ns - 1u : 0u;
+            if (c < (uint32_t)kBuckets) {
+                atomicAdd(&hist[c], 1u);
+            }
+            cls |= c << (8u * v);  // kBuckets (no segment) fits a byte
+            const uint64_t i = base + (uint64_t)threadIdx.x * kPlanV + v;
+            if (i < hi) {
+                mn = min(mn, ns);
+                mx = max(mx, ns);
+                non1 += ns != 1u ? 1u : 0u;
+            }
+            sum += ns;
+        }
+        mine64 += sum;
+        uint32_t excl;
+        const uint32_t tot = block_scan(sum, &excl, wsum);
+        run0 = carry + excl;
+        carry += tot;
+        if (!defer) {
+            tile_words(base, L, run0, true);
+        }
+    };
+#pragma unroll
+    for (uint32_t t = 0; t < kMapRegTiles; ++t) {
+        if (t < ntiles) {
+            count_tile(t, Lr[t], Cr[t], R0[t], true);
+        }
+    }
+    for (uint32_t t = kMapRegTiles; t < ntiles; ++t) {
+        uint32_t L[kPlanV], c, r0;
+        count_tile(t, L, c, r0, false);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
+        mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+        non1 += (uint32_t)__shfl_xor((int)non1, o);
+        full += (uint32_t)__shfl_xor((int)full, o);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mine64 += shfl64(mine64, lane ^ o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(&sh[2], mn);
+        atomicMax(&sh[3], mx);
+        atomicAdd(&sh[1], non1);
+        atomicAdd(&segs64, (unsigned long long)mine64);
+        if (full) {
+            atomicAdd(&hist[c_full], full);
+        }
+    }
+    __syncthreads();
+    // a single-tile block whose messages all have the same segment count
+    // leaves seg_first to the consumers (seg_first_g), as in k_plan
+    const bool write_sf = !one_tile || sh[2] != sh[3];
+    // the register tiles' deferred writes (every exit after the wait runs them)
+    auto deferred = [&]() {
+#pragma unroll
+        for (uint32_t t = 0; t < kMapRegTiles; ++t) {
+            if (t < ntiles) {
+                tile_words(lo + (uint64_t)t * kTile, Lr[t], R0[t], write_sf);
+            }
+        }
+    };
+    // Publish the block words and the histogram, then arrive and wait.
+    PLAN_STAMP(1)
+    if (threadIdx.x < kBuckets) {
+        a.bhist[(uint64_t)bid * kBuckets + threadIdx.x] = hist[threadIdx.x];
+    }
+    if (threadIdx.x == 0) {
+        a.block_sum[bid] = segs64 > kSegLimit ? 0xffffffffu : carry;
+        a.block_sum[nb + bid] = sh[1];
+        a.block_sum[2u * nb + bid] = sh[2] == sh[3] ? sh[2] : 0xffffffffu;
+    }
+    __syncthreads();
+#if BMQCRC_PLAN_DIAG == 1
+    // diagnostic (timing only): no wait and no map; the fold searches seg_first
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(&sync[2], (unsigned long long)ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    deferred();
+    return;
+#endif
+    if (threadIdx.x < 64) {
+        // Arrival: one flag word per block, set to this launch's epoch (a
+        // release store: the block's words above are visible before it, on
+        // every XCD).  No shared counter -- 256 atomics on one word serialize
+        // at the memory side (11-16 us measured,
+        // profiles/r03/ab/planner_phases_counter_wait/) -- and no reset: a
+        // flag of an older launch holds an older epoch.  Wave 0 polls every
+        // block's flag (relaxed loads; one acquire after).
+        if (lane == 0) {
+#if BMQCRC_PLAN_DIAG == 5
+            // diagnostic (timing only, no map, no seginfo stores): no release
+            __hip_atomic_store(&sync[kSyncFlags + bid], (unsigned long long)ep, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+#else
+            __hip_atomic_store(&sync[kSyncFlags + bid], (unsigned long long)ep, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_AGENT);
+#endif
+        }
+        const uint64_t t0 = wall_clock64();
+        uint32_t ok = 1u;
+        static_assert(kPlanMaxBlocks <= 4 * 64, "four flags per lane");
+        while (true) {
+            // all four loads in flight at once (a short-circuit chain made
+            // them four round trips per poll)
+            unsigned long long f[4];
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) {
+                const uint32_t b = (uint32_t)lane + 64u * k;
+                f[k] = b < nb ? __hip_atomic_load(&sync[kSyncFlags + b], __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT)
+                              : (unsigned long long)ep;
+            }
+            const bool mine = f[0] == ep && f[1] == ep && f[2] == ep && f[3] == ep;
+            if (__ballot(!mine) == 0) {
+                break;
+            }
+            if (wall_clock64() - t0 >= a.map_wait_ticks) {
+                ok = 0u;  // not all blocks running: give up the map, keep correctness
+                if (lane == 0 &&
+                    __hip_atomic_exchange(&sync[2], (unsigned long long)ep, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT) != ep) {
+                    // the first block of this launch to give up counts it
+                    __hip_atomic_fetch_add(&sync[3], 1ull, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                }
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+#if BMQCRC_PLAN_DIAG != 5
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
+        if (lane == 0) {
+            go = ok;
+        }
+    }
+    __syncthreads();
+    PLAN_STAMP(2)
+    if (!go) {
+        deferred();
+        return;
+    }
+#if BMQCRC_PLAN_DIAG == 2
+    // diagnostic (timing only): phase 1 and the wait, no map
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(&sync[2], (unsigned long long)ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    deferred();
+    return;
+#endif
+    // Batch shape and size from every block's words: closed-form batches and
+    // those past seginfo's capacity (or 32-bit indices) need no map.
+    // Every load of the other blocks' words goes out at once: the block
+    // words for the shape and size, and this thread's histogram entries for
+    // the class bases below (c = thread % 16, blocks b = thread / 16 + 64 k).
+    static_assert(kPlanBlock % kBuckets == 0 && kPlanMaxBlocks <= 4 * (kPlanBlock / kBuckets),
+                  "bucket-base reduction layout");
+    constexpr uint32_t kParts = kPlanBlock / kBuckets;
+    uint32_t hb[4];
+    {
+        const uint32_t c = threadIdx.x % kBuckets, pi = threadIdx.x / kBuckets;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t b = pi + kParts * k;
+            hb[k] = b < nb ? a.bhist[(uint64_t)b * kBuckets + c] : 0u;
+        }
+    }
+    bool map = true;
+    {
+        const uint32_t j = threadIdx.x;
+        const uint32_t v = j < nb ? a.block_sum[j] : 0u;
+        const uint32_t nn = j < nb ? a.block_sum[nb + j] : 0u;
+        const uint32_t u0 = a.block_sum[2u * nb];
+        const uint32_t u = j < nb ? a.block_sum[2u * nb + j] : u0;
+        const int ragged = __syncthreads_or(nn != 0u);
+        const int mixed = __syncthreads_or(u != u0);
+        if (!ragged || (!mixed && u0 != 0xffffffffu)) {
+            map = false;  // identity or uniform: k_fold uses closed forms
+        } else {
+            unsigned long long sum = v == 0xffffffffu ? (1ull << 40) : v;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                sum += (unsigned long long)shfl64(sum, lane ^ o);
+            }
+            if (lane == 0) {
+                wsum[threadIdx.x >> 6] = (uint32_t)min(sum, (unsigned long long)0xffffffffu);
+            }
+            __syncthreads();
+            unsigned long long all = 0;
+            for (uint32_t w = 0; w < (uint32_t)(kPlanBlock >> 6); ++w) {
+                all += wsum[w];
+            }
+            // past seginfo's capacity: k_fold searches seg_first (or folds
+            // whole messages past 32-bit segment indices)
+            map = all <= min((unsigned long long)a.max_segs, (unsigned long long)kSegLimit);
+        }
+    }
+    if (!map) {
+        deferred();
+        return;
+    }
+    // With the map k_fold never reads seg_first: only out[] is initialised.
+    {
+        const bool keep_sf = BMQCRC_PLAN_DIAG >= 4;  // diag 4, 5 void the map below
+#pragma unroll
+        for (uint32_t t = 0; t < kMapRegTiles; ++t) {
+            if (t < ntiles) {
+                tile_words(lo + (uint64_t)t * kTile, Lr[t], R0[t], keep_sf);
+            }
+        }
+    }
+    // This block's slice of every class (k_plan_sort's bucket-major order).
+    {
+        const uint32_t c = threadIdx.x % kBuckets, pi = threadIdx.x / kBuckets;
+        uint32_t tot = 0, pre = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            tot += hb[k];
+            pre += pi + kParts * k < bid ? hb[k] : 0u;
+        }
+        part[0][pi][c] = tot;
+        part[1][pi][c] = pre;
+        __syncthreads();
+        if (threadIdx.x < kBuckets) {
+            uint32_t t = 0, q = 0;
+            for (uint32_t pp = 0; pp < kParts; ++pp) {
+                t += part[0][pp][threadIdx.x];
+                q += part[1][pp][threadIdx.x];
+            }
+            part[0][0][threadIdx.x] = t;
+            part[1][0][threadIdx.x] = q;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t acc = 0;
+            for (int cc = 0; cc < kBuckets; ++cc) {
+                run[cc] = acc + part[1][0][cc];
+                acc += part[0][0][cc];
+            }
+        }
+        __syncthreads();
+    }
+    // Phase 2: (message, k) of every segment.
+    uint2* const info = (uint2*)a.seginfo;
+    auto write_tile = [&](uint32_t t, const uint32_t (&L)[kPlanV], uint32_t cls) {
+        const uint64_t base = lo + (uint64_t)t * kTile;
+        // Full segments: one claim per wave for all its runs (a wave-wide
+        // exclusive scan of the lanes' counts), so the wave's runs are one
+        // contiguous range, lane by lane.  A lane writes a short run itself;
+        // the wave writes each long run together (coalesced).
+        uint32_t nseg[kPlanV], nf[kPlanV], nf_all = 0;
+#pragma unroll
+        for (uint32_t v = 0; v < kPlanV; ++v) {
+            nseg[v] = segments(L[v]);
+            nf[v] = nseg[v] ? nseg[v] - 1u : 0u;
+            nf_all += nf[v];
+        }
+        uint32_t x = nf_all;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+            if (lane >= o) {
+                x += y;
+            }
+        }
+        const uint32_t tf = (uint32_t)__shfl((int)x, 63);
+        if (tf) {
+            uint32_t pos = 0;
+            if (lane == 0) {
+                pos = atomicAdd(&run[c_full], tf);
+            }
+            pos = (uint32_t)__shfl((int)pos, 0) + (x - nf_all);
+#if BMQCRC_PLAN_DIAG < 4
+            uint32_t at = pos;
+#pragma unroll
+            for (uint32_t v = 0; v < kPlanV; ++v) {
+                if (nf[v] <= kShortRun) {
+                    const uint32_t i = (uint32_t)(base + (uint64_t)threadIdx.x * kPlanV + v);
+                    for (uint32_t k = 0; k < nf[v]; ++k) {
+                        info[at + k] = make_uint2(i, k);
+                    }
+                }
+                at += nf[v];
+            }
+            const uint32_t lane0 = threadIdx.x & ~63u;
+            uint64_t longs = 0;
+#pragma unroll
+            for (uint32_t v = 0; v < kPlanV; ++v) {
+                longs |= __ballot(nf[v] > kShortRun);
+            }
+            for (; longs; longs &= longs - 1ull) {
+                const int src = __builtin_ctzll(longs);
+                uint32_t at2 = (uint32_t)__builtin_amdgcn_readlane((int)pos, src);
+#pragma unroll
+                for (uint32_t v = 0; v < kPlanV; ++v) {
+                    const uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)nf[v], src);
+                    if (n > kShortRun) {
+                        const uint32_t i =
+                            (uint32_t)(base + (uint64_t)(lane0 + (uint32_t)src) * kPlanV + v);
+                        for (uint32_t k = (uint32_t)lane; k < n; k += 64u) {
+                            info[at2 + k] = make_uint2(i, k);
+                        }
+                    }
+                    at2 += n;
+                }
+            }
+#endif
+        }
+        // last (or only) segments: one returning LDS atomic per message
+#pragma unroll
+        for (uint32_t v = 0; v < kPlanV; ++v) {
+            const uint32_t c = (cls >> (8u * v)) & 0xffu;
+            if (c < (uint32_t)kBuckets) {
+                const uint64_t i = base + (uint64_t)threadIdx.x * kPlanV + v;
+                const uint32_t at = atomicAdd(&run[c], 1u);
+#if BMQCRC_PLAN_DIAG < 4
+                info[at] = make_uint2((uint32_t)i, nseg[v] - 1u);
+#else
+                (void)at;
+                (void)i;
+#endif
+            }
+        }
+    };
+#pragma unroll
+    for (uint32_t t = 0; t < kMapRegTiles; ++t) {
+        if (t < ntiles) {
+            write_tile(t, Lr[t], Cr[t]);
+        }
+    }
+    for (uint32_t t = kMapRegTiles; t < ntiles; ++t) {
+        uint32_t L[kPlanV];
+        uint64_t O[kPlanV];
+        load(lo + (uint64_t)t * kTile, L, O);
+        uint32_t cls = 0;
+#pragma unroll
+        for (uint32_t v = 0; v < kPlanV; ++v) {
+            uint32_t c;
+            (void)msg_segments(a, O[v], L[v], seg_shift, &c);
+            cls |= c << (8u * v);
+        }
+        write_tile(t, L, cls);
+    }
+    __syncthreads();
+    PLAN_STAMP(3)
+#if BMQCRC_PLAN_DIAG >= 4
+    // diagnostic (timing only): no seginfo stores, so no map; seg_first written
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(&sync[2], (unsigned long long)ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#endif
+}
+
 // ------------------------------------------------- verify / blob combine
 // Mismatch detection for journal recovery: count and record indices
 // (unordered; the host sorts the short list).
@@ -1644,12 +2223,15 @@ extern "C" int bmqcrc_launch_batch(const BatchArgs* a, void* stream, int num_cus
         return 0;
     }
     if (!a->whole && !a->spec) {
-        if (a->map_planned) {
+        if (a->map_planned && !(a->tune & 128u)) {
+            // ragged batch expected: the single-pass planner (size-class map)
+            hipLaunchKernelGGL(k_plan_map, dim3(a->nblocks), dim3(kPlanBlock), 0, s, *a);
+        } else if (a->map_planned) {
             hipLaunchKernelGGL(k_plan<true>, dim3(a->nblocks), dim3(kPlanBlock), 0, s, *a);
         } else {
             hipLaunchKernelGGL(k_plan<false>, dim3(a->nblocks), dim3(kPlanBlock), 0, s, *a);
         }
-        if (a->map_planned) {
+        if (a->map_planned && (a->tune & 128u)) {
             hipLaunchKernelGGL(k_plan_sort, dim3(a->nblocks), dim3(kPlanBlock), 0, s, *a);
         }
     }
@@ -1684,6 +2266,15 @@ extern "C" int bmqcrc_launch_batch(const BatchArgs* a, void* stream, int num_cus
     }
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
+
+#if BMQCRC_PLAN_DIAG >= 3
+extern "C" __attribute__((visibility("default"))) int bmqcrc_diag_plan_trace(unsigned long long* out)
+{
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_plan_trace), sizeof(g_plan_trace)) == hipSuccess
+               ? 0
+               : -5;
+}
+#endif
 
 extern "C" int bmqcrc_launch_compare(const uint32_t* got, const uint32_t* expected, uint64_t n,
                                      uint32_t* bad_count, uint32_t* bad_idx, uint32_t bad_cap,

@@ -184,6 +184,17 @@ int bmqcrc_last_launch(int device, void* stream, uint32_t* kernels, uint32_t* sp
  * batch differs; a batch still in flight may set the prediction again. */
 int bmqcrc_forget_shape(int device, void* stream);
 
+/* ABI 2.3.  Longest time (microseconds) the blocks of the single-pass
+ * planner (ragged batches) wait for each other on (device, stream) before
+ * giving up the size-class map of that batch; default 1000.  The planner's
+ * blocks meet once, grid-wide; when the GPU cannot run them all at once
+ * (other streams or processes hold the CUs) a block that waited this long
+ * leaves, and the fold then maps segments by binary search -- results are
+ * exact either way, only slower.  0 gives every map up at once (a test hook
+ * for that path).  *voided (may be NULL) receives how many planned batches on
+ * (device, stream) gave up their map so far (read after the stream is idle). */
+int bmqcrc_plan_wait(int device, void* stream, uint64_t wait_us, uint64_t* voided);
+
 /* Zero-copy input: page-lock `bytes` of ordinary host memory at `host` and map
  * it into the GPU address space (hipHostRegister, mapped + portable).
  * *dev_ptr receives the device-side address of `host`; pass it as the arena
@@ -211,7 +222,7 @@ const char* bmqcrc_last_error(void);
 void bmqcrc_note_host_fallback(int32_t rc);
 uint64_t bmqcrc_host_fallbacks(int32_t* last_rc);
 
-/* ABI version: (major << 16) | minor. */
+/* ABI version: (major << 16) | minor (2.3). */
 uint32_t bmqcrc_version(void);
 
 #ifdef __cplusplus

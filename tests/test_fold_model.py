@@ -65,10 +65,25 @@ def fold_stream(words):
     return c
 
 
-def segment_contrib(arena, S, E, mstart, mend, first, seed):
-    L0 = S & ~127
+def geom(S, E, first, ra_lines=1):
+    """k_fold's seg_geom (round 3): when that saves a line or the stream is at
+    most ra_lines lines (kRightAlignLines), the stream is right-aligned at
+    piece granularity -- it ends with the 16-byte piece holding its last byte
+    (or the seed word's) and starts nl lines before, nl the fewest lines that
+    hold pieces [S/16, that piece]; otherwise it starts at S's 128-byte line.
+    Returns (L0, nl)."""
     need_end = max(E, S + 4) if first else E
-    nl = (need_end - L0 + 127) // 128
+    pe = (need_end + 15) & ~15
+    nl_r = (pe - (S & ~15) + 127) // 128
+    L0_l = S & ~127
+    nl_l = (need_end - L0_l + 127) // 128
+    if nl_r < nl_l or nl_r <= ra_lines:
+        return pe - 128 * nl_r, nl_r
+    return L0_l, nl_l
+
+
+def segment_contrib(arena, S, E, mstart, mend, first, seed):
+    L0, nl = geom(S, E, first)
     stream = bytearray(128 * nl)
     lo, hi = S - L0, min(E, L0 + 128 * nl) - L0
     stream[lo:hi] = arena[S:E].tobytes()
@@ -122,9 +137,7 @@ def _segment_pieces(arena, S, E, first, seed, lead_lines):
     in the wave), then the segment's lines, where every 16-byte piece outside
     [S, E) is a zero piece (the DMA reads the zero line) and only the pieces cut
     by S or E are masked byte-exactly; the seed is XORed in last."""
-    L0 = S & ~127
-    need_end = max(E, S + 4) if first else E
-    nl = (need_end - L0 + 127) // 128
+    L0, nl = geom(S, E, first)
     sl, el = S - L0, E - L0
     gS, gE = sl // 16, (el + 15) // 16
     line = bytearray(128 * nl)
@@ -151,9 +164,57 @@ def test_right_aligned_pieces_match_oracle(lead):
         stream, nl = _segment_pieces(arena, off, off + ln, True, seed, lead)
         words = [int(w) for w in np.frombuffer(stream, dtype="<u4")]
         c = fold_stream(words)  # leading zero lines leave a zero-init CRC unchanged
-        padE = (off & ~127) + 128 * nl - (off + ln)
+        L0 = geom(off, off + ln, True)[0]
+        padE = L0 + 128 * nl - (off + ln)
+        if L0 % 128:  # right-aligned: no unshift when E is 16-byte aligned
+            assert 0 <= padE < 16 or ln < 4
         got = G.mulmod_r(c, xpow(-8 * padE)) ^ 0xFFFFFFFF
         assert got == oracle.crc32c(arena[off:off + ln].tobytes(), seed), (off, ln, lead)
+
+
+def test_right_alignment_saves_lines():
+    # a message that straddles a line boundary but fits 128 bytes is one line
+    assert geom(64, 192, True)[1] == 1 and geom(64, 320, True)[1] == 2
+    assert geom(0, 64, True) == (-64, 1)     # one line: right-aligned
+    assert geom(0, 320, True) == (0, 3)      # saves nothing: whole cache lines
+    assert geom(0, 320, True, 1 << 30) == (-64, 3)
+    # never more lines than the 128-byte aligned start of round 2
+    for S in range(0, 300, 7):
+        for ln in range(0, 700, 13):
+            need_end = max(S + ln, S + 4)
+            assert geom(S, S + ln, True)[1] <= (need_end - (S & ~127) + 127) // 128
+
+
+def horner_words(words, skip=0):
+    """k_fold's tail_horner: raw = sum R_d y^(32-d), two words per step,
+    the first `skip` steps not run."""
+    c = 0
+    for d in range(2 * skip, 32):
+        c = mul_y(c ^ words[d])
+    return c
+
+
+def test_one_line_horner_skip():
+    # One-line groups: the remainder is the line, and words before the lowest
+    # S of the wave are zero, so hskip = min(sl) // 8 steps can be skipped.
+    rng = np.random.default_rng(7)
+    arena = rng.integers(0, 256, size=4096, dtype=np.uint8)
+    for _ in range(200):
+        ln = int(rng.integers(0, 129))
+        off = int(rng.integers(0, 3000))
+        seed = int(rng.integers(0, 2**32))
+        stream, nl = _segment_pieces(arena, off, off + ln, True, seed, 0)
+        if nl != 1:
+            continue
+        L0, _ = geom(off, off + ln, True)
+        words = [int(w) for w in np.frombuffer(stream, dtype="<u4")]
+        skip = (off - L0) >> 3
+        assert all(w == 0 for w in words[:2 * skip])
+        c = horner_words(words, skip)
+        assert c == horner_words(words) == fold_stream(words)
+        padE = L0 + 128 - (off + ln)
+        got = G.mulmod_r(c, xpow(-8 * padE)) ^ 0xFFFFFFFF
+        assert got == oracle.crc32c(arena[off:off + ln].tobytes(), seed)
 
 
 # Tap pairing used by k_fold's fold_round / tail_round: adjacent taps (k, k+1)
@@ -312,3 +373,38 @@ def test_move_byte_tables_match_xpow():
             f = G.mulmod_r(f, xb[i][(dist >> (8 * i)) & 0xff])
         # raw CRCs here include the ~0 initial value, which zeros shift too
         assert G.mulmod_r(moved, f) == raw
+
+
+def _table_step(ty, c, r0, r1):
+    """k_fold's horner_step with the header's slicing tables."""
+    v = c ^ r0
+    return (ty[4][v & 255] ^ ty[5][(v >> 8) & 255] ^ ty[6][(v >> 16) & 255] ^ ty[7][v >> 24] ^
+            ty[0][r1 & 255] ^ ty[1][(r1 >> 8) & 255] ^ ty[2][(r1 >> 16) & 255] ^ ty[3][r1 >> 24])
+
+
+def test_two_chain_remainder_matches_horner():
+    """tail_horner2 (round 3): words 0..15 and 16..31 reduced as two chains,
+    raw = c_a * y^16 + c_b with the TY16 tables, equals the one-chain Horner
+    and the model's word-by-word reduction."""
+    flat = _header_table("BMQCRC_TY")
+    ty = [flat[256 * k:256 * (k + 1)] for k in range(8)]
+    f16 = _header_table("BMQCRC_TY16")
+    assert len(f16) == 4 * 256
+    t16 = [f16[256 * k:256 * (k + 1)] for k in range(4)]
+    rng = np.random.default_rng(5)
+    for trial in range(200):
+        R = [int(w) for w in rng.integers(0, 2**32, size=32, dtype=np.uint64)]
+        if trial % 3 == 0:
+            R[:16] = [0] * 16  # the one-line skip case: c_a = 0
+        one = 0
+        for d in range(0, 32, 2):
+            one = _table_step(ty, one, R[d], R[d + 1])
+        ca = cb = 0
+        for d in range(0, 16, 2):
+            ca = _table_step(ty, ca, R[d], R[d + 1])
+            cb = _table_step(ty, cb, R[16 + d], R[17 + d])
+        two = cb ^ t16[0][ca & 255] ^ t16[1][(ca >> 8) & 255] ^ t16[2][(ca >> 16) & 255] ^ \
+            t16[3][ca >> 24]
+        assert one == two == horner_words(R)
+        if trial % 3 == 0:
+            assert cb == one  # tail_horner2<8>

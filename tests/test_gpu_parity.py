@@ -406,6 +406,46 @@ def test_shape_hint_misprediction(cuda):
         run(lens)
 
 
+def test_planner_map_given_up(cuda):
+    # Round 3: ragged batches are planned by one kernel whose blocks meet once,
+    # grid-wide.  When they cannot all run at once a block stops waiting after
+    # bmqcrc_plan_wait's limit and the map is given up: the fold then searches
+    # seg_first.  With the limit at 0 every map is given up; the CRCs must not
+    # change, and the counter must say so.  The default limit maps normally.
+    import torch
+    from blazingmq_amd import plan_wait
+    rng = np.random.default_rng(91)
+    arena_np = rng.integers(0, 256, size=24 << 20, dtype=np.uint8)
+    arena = torch.from_numpy(arena_np).to(cuda)
+    s = torch.cuda.Stream(cuda)
+    lens = np.concatenate([rng.integers(0, 200, size=60000), rng.integers(0, 300000, size=300),
+                           rng.integers(1000, 9000, size=5000)]).astype(np.uint32)
+    rng.shuffle(lens)
+    offs = np.array([rng.integers(0, arena_np.size - l + 1) for l in lens], np.int64)
+    seeds = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64).astype(np.uint32)
+    exp = oracle.batch(arena_np, offs, lens, seeds, nthreads=8)
+
+    def run():
+        got = Crc32c.calculate_batch(arena, torch.from_numpy(offs).to(cuda),
+                                     torch.from_numpy(lens.view(np.int32)).to(cuda),
+                                     torch.from_numpy(seeds.view(np.int32)).to(cuda),
+                                     stream=s, seg_bytes=2048)
+        s.synchronize()
+        bad = np.nonzero(got.cpu().numpy().view(np.uint32) != exp)[0]
+        assert bad.size == 0, [(int(i), int(lens[i])) for i in bad[:8]]
+
+    v0 = plan_wait(cuda.index, s)
+    for _ in range(3):
+        run()
+    assert plan_wait(cuda.index, s, 0) == v0  # a lone stream: every map was kept
+    for _ in range(3):
+        run()
+    v1 = plan_wait(cuda.index, s, 1000)
+    assert v1 > v0
+    run()  # back to mapping
+    assert plan_wait(cuda.index, s) == v1
+
+
 def test_max_length_messages(cuda):
     # The reference's length is an unsigned int (bmqp_crc32c.h:244-246), so the
     # longest message is 2^32 - 1 bytes.  Two such messages (odd offsets,
