@@ -103,7 +103,7 @@ struct DevBuf {
 // Planner + staging scratch for one (device, stream).
 struct Workspace {
     std::mutex mu;
-    DevBuf seg_first, block_sum, seginfo, bhist, plan_sync;
+    DevBuf seg_first, block_sum, seginfo, firstk, bhist, plan_sync;
     uint32_t plan_epoch = 0;  // k_plan_map launches on this workspace (BatchArgs::plan_epoch)
     uint64_t map_wait_ticks = 100000;  // 1 ms (bmqcrc_plan_wait)
 
@@ -235,7 +235,8 @@ int plan_ws(Workspace* w, hipStream_t s, uint64_t n, uint64_t arena_bytes, uint3
     int rc;
     if ((rc = w->seg_first.ensure(4 * std::max<uint64_t>(n, 1))) ||
         (rc = w->block_sum.ensure(12ull * kPlanMaxBlocks)) ||
-        (rc = w->seginfo.ensure(8 * max_segs)) ||
+        (rc = w->seginfo.ensure(4 * max_segs)) ||
+        (rc = w->firstk.ensure(4 * (max_segs / 64 + 2))) ||
         (rc = w->bhist.ensure(4ull * kBuckets * kPlanMaxBlocks)) ||
         (rc = w->plan_sync.ensure(8ull * (kSyncFlags + kPlanMaxBlocks)))) {
         return rc;
@@ -265,8 +266,11 @@ int plan_ws(Workspace* w, hipStream_t s, uint64_t n, uint64_t arena_bytes, uint3
         w->hint_dev = (uint32_t*)d;
     }
     a->shape_hint = w->hint_dev;
-    a->map_planned = 1;
+    // seginfo entries hold 31-bit message indices (bit 31 marks a last
+    // segment): larger batches map their segments by binary search
+    a->map_planned = n < (1ull << 31) ? 1u : 0u;
     a->seg_first = (uint32_t*)w->seg_first.p;
+    a->firstk = (uint32_t*)w->firstk.p;
     a->block_sum = (uint32_t*)w->block_sum.p;
     a->seginfo = (uint32_t*)w->seginfo.p;
     a->bhist = (uint32_t*)w->bhist.p;
@@ -436,7 +440,11 @@ int run_batch(Ctx& c, uint32_t flags, uint32_t seg, const void* arena, uint64_t 
     }
     w->last_spec = a.whole ? 1u : a.spec;
     w->last_seg = a.seg_bytes;
-    w->last_kernels = n == 0 ? 0u : (a.whole || a.spec) ? 1u : a.map_planned ? 3u : 2u;
+    w->last_kernels = n == 0                 ? 0u
+                      : (a.whole || a.spec)  ? 1u
+                      : !a.map_planned       ? 2u
+                      : single_pass_planner(a) ? 2u
+                                             : 3u;
     return 0;
 }
 

@@ -63,7 +63,9 @@ struct BatchArgs {
     uint32_t* block_sum;       // workspace, 3 * nblocks, per k_plan block: [segments |
                                // messages with != 1 segment | segments per message if equal
                                // for all the block's messages, else ~0]
-    uint32_t* seginfo;         // workspace, 2 * max_segs: (message, k) in size-class order
+    uint32_t* seginfo;         // workspace, max_segs: segments in size-class order, one word
+                               // each (message, | kSegLast for its last segment)
+    uint32_t* firstk;          // workspace, max_segs / 64 + 1: k of each group's first entry
     uint32_t* bhist;           // workspace, kBuckets * nblocks: per-block size-class histogram
     uint64_t n;
     uint64_t max_segs;
@@ -96,6 +98,17 @@ struct BatchArgs {
     uint32_t plan_epoch;       // k_plan_map launch tag on this workspace, never 0
     uint64_t map_wait_ticks;   // k_plan_map's grid-wide wait limit (100 MHz wall clock)
 };
+
+constexpr uint32_t kPlanV = 4;  // planner: messages per thread per tile (kPlanBlock * kPlanV)
+constexpr uint32_t kSegLast = 0x80000000u;  // seginfo: the entry is its message's last segment
+
+// Ragged batches (map_planned): the single-pass k_plan_map when its blocks
+// hold more than one tile, else the round-2 pair k_plan<true> + k_plan_sort
+// (TUNE bit 7 forces the pair).
+inline bool single_pass_planner(const BatchArgs& a)
+{
+    return a.per_msg > (uint64_t)kPlanBlock * kPlanV && !(a.tune & 128u);
+}
 
 constexpr uint32_t kHintUnknown = 0;
 constexpr uint32_t kHintClosed = 1;  // uniform segment counts (> 1); | (u << 8) when u divides 64

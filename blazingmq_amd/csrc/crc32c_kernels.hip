@@ -724,14 +724,36 @@ __device__ __forceinline__ SegRef map_segment(const BatchArgs& a, const PlanLds*
             r.msg = seg / uni;
             r.k = seg - r.msg * uni;
         } else if (sorted) {
-            r.msg = a.seginfo[2u * seg];
-            r.k = a.seginfo[2u * seg + 1u];
+            // the raw entry and its group's firstk (resolved in fetch_desc)
+            r.msg = a.seginfo[seg];
+            r.k = a.firstk[(uint32_t)__builtin_amdgcn_readfirstlane((int)seg) >> 6];
         } else {
             r.msg = find_msg(a, pl, seg);  // no map (skipped or overflow): binary search
             r.k = seg - seg_first_g(a, pl, r.msg);
         }
     }
     return r;
+}
+
+// k_fold's sorted map: (message, k) from a group's raw seginfo entries (see
+// put_full / put_last): k = kKFromLength for a last segment, else the lane's
+// distance from its run's head, plus firstk when the run began before the
+// group (its head is lane 0).
+constexpr uint32_t kKFromLength = 0xffffffffu;
+
+__device__ __forceinline__ SegRef resolve_sorted(SegRef r, bool valid)
+{
+    const uint32_t lane = (uint32_t)(threadIdx.x & 63);
+    const uint32_t key = valid ? r.msg : 0xffffffffu;
+    const uint32_t prev = (uint32_t)__shfl_up((int)key, 1);
+    const bool head = lane == 0 || prev != key || (key & kSegLast);
+    const uint64_t heads = __ballot(head);
+    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+    const uint32_t h = 63u - (uint32_t)__builtin_clzll(heads & upto);
+    SegRef o;
+    o.msg = key & ~kSegLast;
+    o.k = (key & kSegLast) ? kKFromLength : (h == 0 ? r.k : 0u) + (lane - h);
+    return o;
 }
 
 __device__ __forceinline__ SegDesc fetch_desc(const BatchArgs& a, SegRef r, bool valid)
@@ -961,7 +983,9 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         if (ONE) {
             setup_lane(valid, d.msg, 0u, 1u, d.off, d.len, d.seed, G);
         } else {
-            setup_lane(valid, d.msg, d.k, nseg, d.off, d.len, d.seed, G);
+            // (a sorted map's last segment: k from the message's length)
+            setup_lane(valid, d.msg, d.k == kKFromLength ? nseg - 1u : d.k, nseg, d.off, d.len,
+                       d.seed, G);
         }
     };
     // Load policy per group: a group of one or two lines per lane (small
@@ -1181,13 +1205,21 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     SegRef ref2 = {0u, 0u};
     if (g < ngroups) {
         const uint32_t s0 = g * 64u + (uint32_t)lane;
-        const SegDesc d0 =
-            identity ? spec
-                     : fetch_desc(a, map_segment(a, &pl, s0, s0 < total, identity, uni, sorted),
-                                  s0 < total);
+        SegRef r0 = {0u, 0u};
+        if (!identity) {
+            r0 = map_segment(a, &pl, s0, s0 < total, identity, uni, sorted);
+            if (sorted) {
+                r0 = resolve_sorted(r0, s0 < total);
+            }
+        }
+        const SegDesc d0 = identity ? spec : fetch_desc(a, r0, s0 < total);
         const uint32_t s1 = (g + stride) * 64u + (uint32_t)lane;
         const bool v1 = g + stride < ngroups && s1 < total;
-        nxt = fetch_desc(a, map_segment(a, &pl, s1, v1, identity, uni, sorted), v1);
+        SegRef r1 = map_segment(a, &pl, s1, v1, identity, uni, sorted);
+        if (sorted) {
+            r1 = resolve_sorted(r1, v1);
+        }
+        nxt = fetch_desc(a, r1, v1);
         const uint32_t s2 = (g + 2u * stride) * 64u + (uint32_t)lane;
         ref2 = map_segment(a, &pl, s2, g + 2u * stride < ngroups && s2 < total, identity, uni,
                            sorted);
@@ -1207,7 +1239,7 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
             setup(nxt, g + stride, G);
             const uint32_t s2 = (g + 2u * stride) * 64u + (uint32_t)lane;
             const bool v2 = g + 2u * stride < ngroups && s2 < total;
-            nxt = fetch_desc(a, ref2, v2);
+            nxt = fetch_desc(a, sorted ? resolve_sorted(ref2, v2) : ref2, v2);
             const uint32_t s3 = (g + 3u * stride) * 64u + (uint32_t)lane;
             ref2 = map_segment(a, &pl, s3, g + 3u * stride < ngroups && s3 < total, identity, uni,
                                sorted);
@@ -1263,7 +1295,6 @@ __device__ __forceinline__ uint32_t msg_segments(const BatchArgs& a, uint64_t of
 // consecutive messages (a tile = 4096 messages, one block scan) and the next
 // tile's lengths are loaded before the current tile is scanned, so a block
 // pays one load latency, not one per tile.
-constexpr uint32_t kPlanV = 4;
 template <bool CLASSES>
 __global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
 {
@@ -1437,6 +1468,26 @@ __device__ __forceinline__ void load_tile(const BatchArgs& a, uint64_t base, uin
     }
 }
 
+// seginfo entries (round 3: 4 bytes per segment, was 8).  A message's last
+// (or only) segment is stored as msg | kSegLast -- k_fold takes k from its
+// length.  A full segment is stored as msg; its k is its distance from the
+// head of its run (a message's full segments are one contiguous run, k
+// ascending), and for a run that began in an earlier group of 64 the k of
+// the group's first entry comes from firstk[group], written here by whoever
+// writes an entry at a multiple of 64.
+__device__ __forceinline__ void put_full(const BatchArgs& a, uint32_t pos, uint32_t msg, uint32_t k)
+{
+    a.seginfo[pos] = msg;
+    if ((pos & 63u) == 0) {
+        a.firstk[pos >> 6] = k;
+    }
+}
+
+__device__ __forceinline__ void put_last(const BatchArgs& a, uint32_t pos, uint32_t msg)
+{
+    a.seginfo[pos] = msg | kSegLast;
+}
+
 // K3 (ragged batches): write (message, k) of every segment into seginfo in
 // size-class order.  Each block fills its slice of every bucket (offsets from
 // K2); a message's non-last segments go to one contiguous run (same class),
@@ -1498,7 +1549,6 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_sort(BatchArgs a)
     const uint32_t SEG = a.seg_bytes;
     const uint32_t seg_shift = (SEG & (SEG - 1u)) == 0 ? (uint32_t)__builtin_ctz(SEG) : 0u;
     const uint32_t c_full = size_class(SEG >> 7);
-    uint2* const info = (uint2*)a.seginfo;
     const uint64_t lo = (uint64_t)blockIdx.x * a.per_msg;
     const uint64_t hi = min(lo + a.per_msg, a.n);
     constexpr uint64_t kTile = (uint64_t)kPlanBlock * kPlanV;
@@ -1521,7 +1571,7 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_sort(BatchArgs a)
                 const uint32_t at = atomicAdd(&run[c_full], nf);
                 const uint32_t i = (uint32_t)(base + (uint64_t)v * kPlanBlock + threadIdx.x);
                 for (uint32_t k = 0; k < nf; ++k) {
-                    info[at + k] = make_uint2(i, k);
+                    put_full(a, at + k, i, k);
                 }
             } else {
                 nf_all += nf;
@@ -1559,7 +1609,7 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_sort(BatchArgs a)
                     const uint32_t i =
                         (uint32_t)(base + (uint64_t)v * kPlanBlock + lane0 + (uint32_t)src);
                     for (uint32_t k = (uint32_t)lane; k < nf; k += 64u) {
-                        info[at + k] = make_uint2(i, k);
+                        put_full(a, at + k, i, k);
                     }
                     at += nf;
                 }
@@ -1573,7 +1623,7 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_sort(BatchArgs a)
         for (uint32_t v = 0; v < kPlanV; ++v) {
             if (c[v] < (uint32_t)kBuckets) {
                 const uint64_t i = base + (uint64_t)v * kPlanBlock + threadIdx.x;
-                info[atomicAdd(&run[c[v]], 1u)] = make_uint2((uint32_t)i, nseg[v] - 1u);
+                put_last(a, atomicAdd(&run[c[v]], 1u), (uint32_t)i);
             }
         }
     }
@@ -1609,6 +1659,9 @@ constexpr uint32_t kMapRegTiles = BMQCRC_MAP_REG_TILES;  // tiles kept in regist
 #ifndef BMQCRC_PLAN_DIAG
 #define BMQCRC_PLAN_DIAG 0  // timing diagnostics only (see below); the product is built with 0
 #endif
+#ifndef BMQCRC_PLAN_PHIST
+#define BMQCRC_PLAN_PHIST 0  // 1: per-thread class counters instead of LDS atomics (A/B)
+#endif
 
 #if BMQCRC_PLAN_DIAG >= 3
 // diagnostic build only: per-block wall-clock stamps of the last launch
@@ -1632,6 +1685,16 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
     __shared__ uint32_t part[2][kPlanBlock / kBuckets][kBuckets];
     __shared__ unsigned long long segs64;
     __shared__ uint32_t go;
+#if BMQCRC_PLAN_PHIST
+    // per-thread class counters, two 16-bit halves per word, [class/2][thread]:
+    // each thread adds to its own column (bank = thread), no same-address
+    // atomics (a wave's 64 messages mostly share one or two classes)
+    __shared__ uint32_t phist[kBuckets / 2][kPlanBlock];
+#pragma unroll
+    for (int r = 0; r < kBuckets / 2; ++r) {
+        phist[r][threadIdx.x] = 0u;
+    }
+#endif
     const uint32_t nb = a.nblocks, ep = a.plan_epoch, bid = blockIdx.x;
     unsigned long long* const sync = a.plan_sync;
     if (threadIdx.x == 0) {
@@ -1718,7 +1781,11 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
             const uint32_t ns = msg_segments(a, O[v], L[v], seg_shift, &c);
             full += ns ? ns - 1u : 0u;
             if (c < (uint32_t)kBuckets) {
+#if BMQCRC_PLAN_PHIST
+                phist[c >> 1][threadIdx.x] += 1u << (16u * (c & 1u));
+#else
                 atomicAdd(&hist[c], 1u);
+#endif
             }
             cls |= c << (8u * v);  // kBuckets (no segment) fits a byte
             const uint64_t i = base + (uint64_t)threadIdx.x * kPlanV + v;
@@ -1759,6 +1826,30 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
     for (int o = 32; o > 0; o >>= 1) {
         mine64 += shfl64(mine64, lane ^ o);
     }
+#if BMQCRC_PLAN_PHIST
+    {
+        // row r = thread / 128 sums 8 columns of its 128-thread slice, then
+        // both halves are reduced over the wave and added once per wave
+        __syncthreads();
+        const uint32_t r = threadIdx.x >> 7, c0 = (threadIdx.x & 127u) * 8u;
+        uint32_t hlo = 0, hhi = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) {
+            const uint32_t w = phist[r][c0 + k];
+            hlo += w & 0xffffu;
+            hhi += w >> 16;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            hlo += (uint32_t)__shfl_xor((int)hlo, o);
+            hhi += (uint32_t)__shfl_xor((int)hhi, o);
+        }
+        if (lane == 0) {
+            atomicAdd(&hist[2u * r], hlo);
+            atomicAdd(&hist[2u * r + 1u], hhi);
+        }
+    }
+#endif
     if ((threadIdx.x & 63) == 0) {
         atomicMin(&sh[2], mn);
         atomicMax(&sh[3], mx);
@@ -1963,7 +2054,6 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
         __syncthreads();
     }
     // Phase 2: (message, k) of every segment.
-    uint2* const info = (uint2*)a.seginfo;
     auto write_tile = [&](uint32_t t, const uint32_t (&L)[kPlanV], uint32_t cls) {
         const uint64_t base = lo + (uint64_t)t * kTile;
         // Full segments: one claim per wave for all its runs (a wave-wide
@@ -1999,7 +2089,7 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
                 if (nf[v] <= kShortRun) {
                     const uint32_t i = (uint32_t)(base + (uint64_t)threadIdx.x * kPlanV + v);
                     for (uint32_t k = 0; k < nf[v]; ++k) {
-                        info[at + k] = make_uint2(i, k);
+                        put_full(a, at + k, i, k);
                     }
                 }
                 at += nf[v];
@@ -2020,7 +2110,7 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
                         const uint32_t i =
                             (uint32_t)(base + (uint64_t)(lane0 + (uint32_t)src) * kPlanV + v);
                         for (uint32_t k = (uint32_t)lane; k < n; k += 64u) {
-                            info[at2 + k] = make_uint2(i, k);
+                            put_full(a, at2 + k, i, k);
                         }
                     }
                     at2 += n;
@@ -2036,7 +2126,7 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
                 const uint64_t i = base + (uint64_t)threadIdx.x * kPlanV + v;
                 const uint32_t at = atomicAdd(&run[c], 1u);
 #if BMQCRC_PLAN_DIAG < 4
-                info[at] = make_uint2((uint32_t)i, nseg[v] - 1u);
+                put_last(a, at, (uint32_t)i);
 #else
                 (void)at;
                 (void)i;
@@ -2223,15 +2313,21 @@ extern "C" int bmqcrc_launch_batch(const BatchArgs* a, void* stream, int num_cus
         return 0;
     }
     if (!a->whole && !a->spec) {
-        if (a->map_planned && !(a->tune & 128u)) {
-            // ragged batch expected: the single-pass planner (size-class map)
+        // Ragged batch expected: the single-pass planner when its blocks
+        // hold more than one tile (it keeps them in registers across its
+        // grid-wide wait instead of reloading them); with one tile per block
+        // the round-2 pair is as fast (Zipf's 1/8 shard: 26.5 against 27.8
+        // us traced; the whole batch 75.3 against 70.2 us,
+        // profiles/r03/ab/planner_traces.txt).
+        const bool single_pass = single_pass_planner(*a);
+        if (a->map_planned && single_pass) {
             hipLaunchKernelGGL(k_plan_map, dim3(a->nblocks), dim3(kPlanBlock), 0, s, *a);
         } else if (a->map_planned) {
             hipLaunchKernelGGL(k_plan<true>, dim3(a->nblocks), dim3(kPlanBlock), 0, s, *a);
         } else {
             hipLaunchKernelGGL(k_plan<false>, dim3(a->nblocks), dim3(kPlanBlock), 0, s, *a);
         }
-        if (a->map_planned && (a->tune & 128u)) {
+        if (a->map_planned && !single_pass) {
             hipLaunchKernelGGL(k_plan_sort, dim3(a->nblocks), dim3(kPlanBlock), 0, s, *a);
         }
     }

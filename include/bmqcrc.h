@@ -171,8 +171,9 @@ int bmqcrc_fill_synthetic(void* dev_dst, uint64_t nbytes, uint64_t seed, uint64_
 int bmqcrc_kernel_timing(int device, void* stream, double* total_ms, uint32_t* count);
 
 /* ABI 2.2.  Launch plan of the previous batch CRC'd on (device, stream):
- * *kernels = kernels it launched (1: the fold alone; 2: planner + fold; 3:
- * planner, size-class sort, fold), *spec = the segments per message its single
+ * *kernels = kernels it launched (1: the fold alone; 2: planner + fold, the
+ * planner being the single-pass size-class map for large ragged batches
+ * (ABI 2.3); 3: planner, size-class sort, fold), *spec = the segments per message its single
  * launch assumed (0: planned; 1 also for BMQCRC_F_WHOLE_MESSAGES), *seg_bytes =
  * the segment size used.  Any pointer may be NULL. */
 int bmqcrc_last_launch(int device, void* stream, uint32_t* kernels, uint32_t* spec,

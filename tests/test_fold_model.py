@@ -408,3 +408,52 @@ def test_two_chain_remainder_matches_horner():
         assert one == two == horner_words(R)
         if trial % 3 == 0:
             assert cb == one  # tail_horner2<8>
+
+
+def _decode_groups(entries, firstk):
+    """k_fold's resolve_sorted over every group of 64 entries."""
+    LAST = 0x80000000
+    out = []
+    for g in range(0, len(entries), 64):
+        grp = entries[g:g + 64]
+        head = []
+        for l, e in enumerate(grp):
+            head.append(l == 0 or grp[l - 1] != e or bool(e & LAST))
+        for l, e in enumerate(grp):
+            h = max(j for j in range(l + 1) if head[j])
+            if e & LAST:
+                out.append((e & ~LAST, None))  # k from the message's length
+            else:
+                out.append((e, (firstk[g >> 6] if h == 0 else 0) + (l - h)))
+    return out
+
+
+def test_four_byte_seginfo_round_trip():
+    """Round 3's seginfo encoding (put_full / put_last / resolve_sorted): runs of
+    full segments written contiguously in k order, last segments flagged, and
+    firstk written for entries at multiples of 64 -- decoding every group
+    recovers (message, k) exactly, for runs of any length at any offset."""
+    rng = np.random.default_rng(23)
+    for trial in range(40):
+        nmsg = int(rng.integers(1, 300))
+        nseg = [int(x) for x in rng.choice([1, 1, 1, 2, 3, 9, 40, 200], size=nmsg)]
+        full = [(m, k) for m in range(nmsg) for k in range(nseg[m] - 1)]
+        last = [(m, nseg[m] - 1) for m in range(nmsg)]
+        order = rng.permutation(nmsg)
+        # classes: full segments in one region (runs contiguous), last ones elsewhere,
+        # shuffled among themselves (LDS-atomic claim order)
+        entries, firstk, want = [], {}, []
+        for m in order:
+            for k in range(nseg[m] - 1):
+                pos = len(entries)
+                entries.append(int(m))
+                if pos % 64 == 0:
+                    firstk[pos >> 6] = k
+                want.append((int(m), k))
+        for j in rng.permutation(len(last)):
+            m, k = last[j]
+            entries.append(int(m) | 0x80000000)
+            want.append((int(m), None))
+        got = _decode_groups(entries, firstk)
+        assert got == want
+        assert len(full) + len(last) == len(entries)

@@ -413,15 +413,18 @@ def test_planner_map_given_up(cuda):
     # seg_first.  With the limit at 0 every map is given up; the CRCs must not
     # change, and the counter must say so.  The default limit maps normally.
     import torch
-    from blazingmq_amd import plan_wait
+    from blazingmq_amd import last_launch, plan_wait
     rng = np.random.default_rng(91)
-    arena_np = rng.integers(0, 256, size=24 << 20, dtype=np.uint8)
+    arena_np = rng.integers(0, 256, size=64 << 20, dtype=np.uint8)
     arena = torch.from_numpy(arena_np).to(cuda)
     s = torch.cuda.Stream(cuda)
-    lens = np.concatenate([rng.integers(0, 200, size=60000), rng.integers(0, 300000, size=300),
+    # more than four planner tiles per block (> 1.3M messages): the
+    # single-pass planner, not the round-2 pair
+    lens = np.concatenate([rng.integers(0, 200, size=1_400_000),
+                           rng.integers(0, 300000, size=300),
                            rng.integers(1000, 9000, size=5000)]).astype(np.uint32)
     rng.shuffle(lens)
-    offs = np.array([rng.integers(0, arena_np.size - l + 1) for l in lens], np.int64)
+    offs = (rng.random(lens.size) * (arena_np.size - lens + 1)).astype(np.int64)
     seeds = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64).astype(np.uint32)
     exp = oracle.batch(arena_np, offs, lens, seeds, nthreads=8)
 
@@ -437,6 +440,7 @@ def test_planner_map_given_up(cuda):
     v0 = plan_wait(cuda.index, s)
     for _ in range(3):
         run()
+    assert last_launch(cuda.index, s)["kernels"] == 2  # k_plan_map + k_fold
     assert plan_wait(cuda.index, s, 0) == v0  # a lone stream: every map was kept
     for _ in range(3):
         run()
@@ -444,6 +448,37 @@ def test_planner_map_given_up(cuda):
     assert v1 > v0
     run()  # back to mapping
     assert plan_wait(cuda.index, s) == v1
+
+
+def test_planners_on_two_streams_at_once(cuda):
+    # Two large ragged batches enqueued on two streams without waiting: their
+    # single-pass planners may share the GPU, so a planner's blocks may not
+    # all be resident together and a block may give its map up (exact either
+    # way).  Every CRC of both batches must match, with and without a wait
+    # limit that forces the give-up.
+    import torch
+    from blazingmq_amd import plan_wait
+    rng = np.random.default_rng(92)
+    arena_np = rng.integers(0, 256, size=64 << 20, dtype=np.uint8)
+    arena = torch.from_numpy(arena_np).to(cuda)
+    streams = [torch.cuda.Stream(cuda), torch.cuda.Stream(cuda)]
+    batches = []
+    for j in range(2):
+        lens = np.concatenate([rng.integers(0, 300, size=1_400_000),
+                               rng.integers(0, 200000, size=200 + 100 * j)]).astype(np.uint32)
+        rng.shuffle(lens)
+        offs = (rng.random(lens.size) * (arena_np.size - lens + 1)).astype(np.int64)
+        batches.append((torch.from_numpy(offs).to(cuda), torch.from_numpy(lens.view(np.int32)).to(cuda),
+                        oracle.batch(arena_np, offs, lens, None, nthreads=8)))
+    torch.cuda.synchronize(cuda)
+    for wait_us in (1000, 0, 1000):
+        for s in streams:
+            plan_wait(cuda.index, s, wait_us)
+        outs = [Crc32c.calculate_batch(arena, o, ln, None, stream=s, sync=False)
+                for (o, ln, _), s in zip(batches, streams)]
+        torch.cuda.synchronize(cuda)
+        for (_, _, exp), got in zip(batches, outs):
+            assert np.array_equal(got.cpu().numpy().view(np.uint32), exp)
 
 
 def test_max_length_messages(cuda):

@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 L=blazingmq_amd/lib
 cp $L/libbmqcrc.so /tmp/pd3_base.so
 rc=0
-for v in pd3 pd4 pd5; do
+for v in pd3 pd4 pd5 pd3h; do
   cp $L/variant_$v.so $L/libbmqcrc.so
   for s in 0/1 7/8; do
     echo "{\"variant\": \"$v\"}" >> gpurun_out/pd3.jsonl
