@@ -52,6 +52,17 @@ constexpr bool kRightAlign = BMQCRC_RIGHT_ALIGN != 0;  // 0: round 2's 128-byte 
 #define BMQCRC_SPLIT_HORNER 0
 #endif
 constexpr bool kSplitHorner = BMQCRC_SPLIT_HORNER != 0;
+// A/B knobs: one-line groups read their line without a zeroed tap array
+// (kSplitTail); raised wave priority while a group sets up and issues the
+// next group's loads (kPrioIssue).
+#ifndef BMQCRC_SPLIT_TAIL
+#define BMQCRC_SPLIT_TAIL 0
+#endif
+constexpr bool kSplitTail = BMQCRC_SPLIT_TAIL != 0;
+#ifndef BMQCRC_PRIO_ISSUE
+#define BMQCRC_PRIO_ISSUE 0
+#endif
+constexpr bool kPrioIssue = BMQCRC_PRIO_ISSUE != 0;
 
 struct BatchArgs {
     const uint8_t* arena;      // device

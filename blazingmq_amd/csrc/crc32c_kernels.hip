@@ -1055,6 +1055,26 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         // ring, so they are summed before the last line lands, and the path
         // from its arrival to the next group's loads is 32 XORs (one-line
         // streams: no history)
+        if (kSplitTail) {
+            // one-line streams read the line as is; the others XOR the taps
+            // (two copies of the line read, so that no zeroed H is
+            // materialised for every group: 32 VALU per group)
+            if (R == 1) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                load_line(0u, slot, Rm);
+                return;
+            }
+            uint32_t H[32];
+            tail_taps(q, p, H);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            uint32_t m[32];
+            load_line(R - 1u, slot, m);
+#pragma unroll
+            for (int d = 0; d < 32; ++d) {
+                Rm[d] = m[d] ^ H[d];
+            }
+            return;
+        }
         uint32_t H[32];
         if (R == 1) {
 #pragma unroll
@@ -1233,6 +1253,9 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         // they load while this group's remainder is reduced and combined.
         const Group C = G;
         if (g + stride < ngroups) {
+            if (kPrioIssue) {
+                __builtin_amdgcn_s_setprio(2);  // the next loads out first
+            }
             // setup first: it reads the descriptors loaded a group ago, and the
             // compiler's wait for them (which cannot see the DMA waits above)
             // must not also wait for the loads issued next
@@ -1244,6 +1267,9 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
             ref2 = map_segment(a, &pl, s3, g + 3u * stride < ngroups && s3 < total, identity, uni,
                                sorted);
             issue_first_rounds(G);
+            if (kPrioIssue) {
+                __builtin_amdgcn_s_setprio(0);
+            }
         }
         if (ONE && kSplitHorner) {
             finish(C, C.hskip ? tail_horner2<8>(Rm, tab_lds, xb_lds)
