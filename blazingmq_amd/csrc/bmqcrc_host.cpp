@@ -217,11 +217,18 @@ uint64_t max_segs_for(uint64_t n, uint64_t arena_bytes, uint32_t seg)
     return n + arena_bytes / seg + 64;
 }
 
-// Contiguous ranges of whole kPlanBlock tiles, at most kPlanMaxBlocks blocks.
+// Contiguous ranges of whole kPlanBlock tiles, at most kPlanMaxBlocks blocks
+// (and at least kPlanMinTiles tiles per block while that leaves >= 32 blocks).
+#ifndef BMQCRC_PLAN_MIN_TILES
+#define BMQCRC_PLAN_MIN_TILES 1
+#endif
+constexpr uint64_t kPlanMinTiles = BMQCRC_PLAN_MIN_TILES;
+
 static void split_ranges(uint64_t items, uint64_t* per, uint32_t* blocks)
 {
     const uint64_t tiles = std::max<uint64_t>((items + kPlanBlock - 1) / kPlanBlock, 1);
-    const uint64_t nb = std::min<uint64_t>(tiles, kPlanMaxBlocks);
+    const uint64_t min_tiles = std::min<uint64_t>(kPlanMinTiles, std::max<uint64_t>(tiles / 32, 1));
+    const uint64_t nb = std::min<uint64_t>((tiles + min_tiles - 1) / min_tiles, kPlanMaxBlocks);
     const uint64_t tiles_per = (tiles + nb - 1) / nb;
     *per = tiles_per * kPlanBlock;
     *blocks = (uint32_t)((tiles + tiles_per - 1) / tiles_per);
@@ -1569,8 +1576,10 @@ int bmqcrc_plan_wait(int device, void* stream, uint64_t wait_us, uint64_t* voide
     if (voided) {
         // k_plan_map counts its launches that gave up their map (plan_sync[3])
         unsigned long long n = 0;
-        if (w->plan_sync.p) {
-            HIP_TRY(hipMemcpy(&n, (const uint8_t*)w->plan_sync.p + 24, 8, hipMemcpyDeviceToHost));
+        if (w->plan_sync.p) {  // after the work already enqueued on this stream
+            HIP_TRY(hipMemcpyAsync(&n, (const uint8_t*)w->plan_sync.p + 24, 8,
+                                   hipMemcpyDeviceToHost, (hipStream_t)stream));
+            HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
         }
         *voided = n;
     }

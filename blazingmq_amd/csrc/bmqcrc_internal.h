@@ -47,22 +47,6 @@ constexpr uint32_t kRightAlignLines = BMQCRC_RIGHT_ALIGN_LINES;
 #define BMQCRC_RIGHT_ALIGN 1
 #endif
 constexpr bool kRightAlign = BMQCRC_RIGHT_ALIGN != 0;  // 0: round 2's 128-byte aligned streams
-// The ONE kernel's remainder step as two independent chains (A/B knob).
-#ifndef BMQCRC_SPLIT_HORNER
-#define BMQCRC_SPLIT_HORNER 0
-#endif
-constexpr bool kSplitHorner = BMQCRC_SPLIT_HORNER != 0;
-// A/B knobs: one-line groups read their line without a zeroed tap array
-// (kSplitTail); raised wave priority while a group sets up and issues the
-// next group's loads (kPrioIssue).
-#ifndef BMQCRC_SPLIT_TAIL
-#define BMQCRC_SPLIT_TAIL 0
-#endif
-constexpr bool kSplitTail = BMQCRC_SPLIT_TAIL != 0;
-#ifndef BMQCRC_PRIO_ISSUE
-#define BMQCRC_PRIO_ISSUE 0
-#endif
-constexpr bool kPrioIssue = BMQCRC_PRIO_ISSUE != 0;
 
 struct BatchArgs {
     const uint8_t* arena;      // device

@@ -56,7 +56,6 @@ __constant__ uint32_t c_x2col[31][32] = BMQCRC_X2COL;
 __constant__ uint32_t c_xneg8[136] = BMQCRC_XNEG8;
 __constant__ uint32_t c_xbytes[4][256] = BMQCRC_XBYTES;
 __constant__ uint32_t c_ty[8][256] = BMQCRC_TY;
-__constant__ uint32_t c_ty16[4][256] = BMQCRC_TY16;
 
 // All-zero line in device memory: the LDS-DMA source of every 16-byte piece
 // that lies outside a segment's bytes, and of every round outside its stream.
@@ -341,43 +340,6 @@ __device__ __forceinline__ uint32_t tail_horner(const uint32_t (&R)[32], uint32_
         c = xor3(hi, lo, tab_lookup(tab_lds, 7, v >> 24) ^ tab_lookup(tab_lds, 3, w >> 24));
     }
     return c;
-}
-
-// Two independent chains (round 3, kSplitHorner): words 0..15 and 16..31 are
-// reduced side by side, c_a = sum_{d<16} R_d y^(16-d) and c_b = sum_{d>=16}
-// R_d y^(32-d), then raw = c_a * y^16 + c_b (four lookups in TY16 tables,
-// LDS at t16_lds).  Eight dependent steps instead of sixteen.
-__device__ __forceinline__ uint32_t horner_step(uint32_t c, uint32_t r0, uint32_t r1,
-                                                uint32_t tab_lds)
-{
-    const uint32_t v = c ^ r0;
-    const uint32_t hi = xor3(tab_lookup(tab_lds, 4, v & 0xffu),
-                             tab_lookup(tab_lds, 5, (v >> 8) & 0xffu),
-                             tab_lookup(tab_lds, 6, (v >> 16) & 0xffu));
-    const uint32_t lo = xor3(tab_lookup(tab_lds, 0, r1 & 0xffu),
-                             tab_lookup(tab_lds, 1, (r1 >> 8) & 0xffu),
-                             tab_lookup(tab_lds, 2, (r1 >> 16) & 0xffu));
-    return xor3(hi, lo, tab_lookup(tab_lds, 7, v >> 24) ^ tab_lookup(tab_lds, 3, r1 >> 24));
-}
-
-template <int SKIP>
-__device__ __forceinline__ uint32_t tail_horner2(const uint32_t (&R)[32], uint32_t tab_lds,
-                                                 uint32_t t16_lds)
-{
-    static_assert(SKIP == 0 || SKIP == 8, "two chains: all words, or the second half");
-    uint32_t ca = 0, cb = 0;
-#pragma unroll
-    for (int d = 0; d < 16; d += 2) {
-        if (SKIP == 0) {
-            ca = horner_step(ca, R[d], R[d + 1], tab_lds);
-        }
-        cb = horner_step(cb, R[16 + d], R[17 + d], tab_lds);
-    }
-    if (SKIP == 8) {
-        return cb;
-    }
-    return cb ^ xor3(tab_lookup(t16_lds, 0, ca & 0xffu), tab_lookup(t16_lds, 1, (ca >> 8) & 0xffu),
-                     tab_lookup(t16_lds, 2, (ca >> 16) & 0xffu) ^ tab_lookup(t16_lds, 3, ca >> 24));
 }
 
 // Word w (0..31) of this lane's 128-byte line in an LDS slot (the pieces are
@@ -775,10 +737,7 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
 {
     // remainder tables, DMA slots, move factors (not needed by ONE: no moves
     // in its first pass)
-    // (the ONE kernel keeps the y^16 tables of the two-chain remainder step
-    // where the others keep the move factors)
-    __shared__ __attribute__((aligned(16))) uint8_t
-        lds[kTabBytes + kLdsBytes + ((ONE && !kSplitHorner) ? 0 : kXbBytes)];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kTabBytes + kLdsBytes + (ONE ? 0 : kXbBytes)];
 
     const int lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -799,11 +758,11 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     }
     static_assert(4 * 256 == 4 * kWavesPerBlock * 64, "move factors: 4 words per thread");
     uint32_t xw[4];
-    if (!ONE || kSplitHorner) {
+    if (!ONE) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const uint32_t t = threadIdx.x + (uint32_t)i * (kWavesPerBlock * 64);
-            xw[i] = ONE ? c_ty16[t >> 8][t & 255u] : c_xbytes[t >> 8][t & 255u];
+            xw[i] = c_xbytes[t >> 8][t & 255u];
         }
     }
     const uint32_t whole = ONE ? 0u : a.whole;
@@ -836,7 +795,7 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     if (threadIdx.x < 136u) {
         xneg8[threadIdx.x] = xn;
     }
-    if (!ONE || kSplitHorner) {
+    if (!ONE) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const uint32_t t = threadIdx.x + (uint32_t)i * (kWavesPerBlock * 64);
@@ -1055,35 +1014,17 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         // ring, so they are summed before the last line lands, and the path
         // from its arrival to the next group's loads is 32 XORs (one-line
         // streams: no history)
-        if (kSplitTail) {
-            // one-line streams read the line as is; the others XOR the taps
-            // (two copies of the line read, so that no zeroed H is
-            // materialised for every group: 32 VALU per group)
-            if (R == 1) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                load_line(0u, slot, Rm);
-                return;
-            }
-            uint32_t H[32];
-            tail_taps(q, p, H);
+        // one-line streams read the line as is; the others XOR the taps into
+        // the last line (no zeroed tap array for one-line groups: materialised
+        // for every group it cost 32 VALU each, 1M x 256 B +1.8 %, 64 B +3 %,
+        // profiles/r03/ab/ab7_split_tail_priority.jsonl)
+        if (R == 1) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            uint32_t m[32];
-            load_line(R - 1u, slot, m);
-#pragma unroll
-            for (int d = 0; d < 32; ++d) {
-                Rm[d] = m[d] ^ H[d];
-            }
+            load_line(0u, slot, Rm);
             return;
         }
         uint32_t H[32];
-        if (R == 1) {
-#pragma unroll
-            for (int d = 0; d < 32; ++d) {
-                H[d] = 0u;
-            }
-        } else {
-            tail_taps(q, p, H);
-        }
+        tail_taps(q, p, H);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         uint32_t m[32];
         load_line(R - 1u, slot, m);
@@ -1253,9 +1194,6 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         // they load while this group's remainder is reduced and combined.
         const Group C = G;
         if (g + stride < ngroups) {
-            if (kPrioIssue) {
-                __builtin_amdgcn_s_setprio(2);  // the next loads out first
-            }
             // setup first: it reads the descriptors loaded a group ago, and the
             // compiler's wait for them (which cannot see the DMA waits above)
             // must not also wait for the loads issued next
@@ -1267,16 +1205,8 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
             ref2 = map_segment(a, &pl, s3, g + 3u * stride < ngroups && s3 < total, identity, uni,
                                sorted);
             issue_first_rounds(G);
-            if (kPrioIssue) {
-                __builtin_amdgcn_s_setprio(0);
-            }
         }
-        if (ONE && kSplitHorner) {
-            finish(C, C.hskip ? tail_horner2<8>(Rm, tab_lds, xb_lds)
-                              : tail_horner2<0>(Rm, tab_lds, xb_lds));
-        } else {
-            finish(C, C.hskip ? tail_horner<8>(Rm, tab_lds) : tail_horner(Rm, tab_lds));
-        }
+        finish(C, C.hskip ? tail_horner<8>(Rm, tab_lds) : tail_horner(Rm, tab_lds));
     }
     if (spec_mode && long_seen) {
         second_pass();
@@ -1683,10 +1613,8 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_sort(BatchArgs a)
 #endif
 constexpr uint32_t kMapRegTiles = BMQCRC_MAP_REG_TILES;  // tiles kept in registers across the wait
 #ifndef BMQCRC_PLAN_DIAG
-#define BMQCRC_PLAN_DIAG 0  // timing diagnostics only (see below); the product is built with 0
-#endif
-#ifndef BMQCRC_PLAN_PHIST
-#define BMQCRC_PLAN_PHIST 0  // 1: per-thread class counters instead of LDS atomics (A/B)
+#define BMQCRC_PLAN_DIAG 0  // 3: per-block phase stamps, 4: the same without seginfo stores
+                            // (timing diagnostics, tools/plan_trace_diag.py); product: 0
 #endif
 
 #if BMQCRC_PLAN_DIAG >= 3
@@ -1711,16 +1639,6 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
     __shared__ uint32_t part[2][kPlanBlock / kBuckets][kBuckets];
     __shared__ unsigned long long segs64;
     __shared__ uint32_t go;
-#if BMQCRC_PLAN_PHIST
-    // per-thread class counters, two 16-bit halves per word, [class/2][thread]:
-    // each thread adds to its own column (bank = thread), no same-address
-    // atomics (a wave's 64 messages mostly share one or two classes)
-    __shared__ uint32_t phist[kBuckets / 2][kPlanBlock];
-#pragma unroll
-    for (int r = 0; r < kBuckets / 2; ++r) {
-        phist[r][threadIdx.x] = 0u;
-    }
-#endif
     const uint32_t nb = a.nblocks, ep = a.plan_epoch, bid = blockIdx.x;
     unsigned long long* const sync = a.plan_sync;
     if (threadIdx.x == 0) {
@@ -1807,11 +1725,7 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
             const uint32_t ns = msg_segments(a, O[v], L[v], seg_shift, &c);
             full += ns ? ns - 1u : 0u;
             if (c < (uint32_t)kBuckets) {
-#if BMQCRC_PLAN_PHIST
-                phist[c >> 1][threadIdx.x] += 1u << (16u * (c & 1u));
-#else
                 atomicAdd(&hist[c], 1u);
-#endif
             }
             cls |= c << (8u * v);  // kBuckets (no segment) fits a byte
             const uint64_t i = base + (uint64_t)threadIdx.x * kPlanV + v;
@@ -1852,30 +1766,6 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
     for (int o = 32; o > 0; o >>= 1) {
         mine64 += shfl64(mine64, lane ^ o);
     }
-#if BMQCRC_PLAN_PHIST
-    {
-        // row r = thread / 128 sums 8 columns of its 128-thread slice, then
-        // both halves are reduced over the wave and added once per wave
-        __syncthreads();
-        const uint32_t r = threadIdx.x >> 7, c0 = (threadIdx.x & 127u) * 8u;
-        uint32_t hlo = 0, hhi = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < 8; ++k) {
-            const uint32_t w = phist[r][c0 + k];
-            hlo += w & 0xffffu;
-            hhi += w >> 16;
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            hlo += (uint32_t)__shfl_xor((int)hlo, o);
-            hhi += (uint32_t)__shfl_xor((int)hhi, o);
-        }
-        if (lane == 0) {
-            atomicAdd(&hist[2u * r], hlo);
-            atomicAdd(&hist[2u * r + 1u], hhi);
-        }
-    }
-#endif
     if ((threadIdx.x & 63) == 0) {
         atomicMin(&sh[2], mn);
         atomicMax(&sh[3], mx);
@@ -1909,14 +1799,6 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
         a.block_sum[2u * nb + bid] = sh[2] == sh[3] ? sh[2] : 0xffffffffu;
     }
     __syncthreads();
-#if BMQCRC_PLAN_DIAG == 1
-    // diagnostic (timing only): no wait and no map; the fold searches seg_first
-    if (threadIdx.x == 0) {
-        __hip_atomic_store(&sync[2], (unsigned long long)ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    deferred();
-    return;
-#endif
     if (threadIdx.x < 64) {
         // Arrival: one flag word per block, set to this launch's epoch (a
         // release store: the block's words above are visible before it, on
@@ -1926,14 +1808,8 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
         // flag of an older launch holds an older epoch.  Wave 0 polls every
         // block's flag (relaxed loads; one acquire after).
         if (lane == 0) {
-#if BMQCRC_PLAN_DIAG == 5
-            // diagnostic (timing only, no map, no seginfo stores): no release
-            __hip_atomic_store(&sync[kSyncFlags + bid], (unsigned long long)ep, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-#else
             __hip_atomic_store(&sync[kSyncFlags + bid], (unsigned long long)ep, __ATOMIC_RELEASE,
                                __HIP_MEMORY_SCOPE_AGENT);
-#endif
         }
         const uint64_t t0 = wall_clock64();
         uint32_t ok = 1u;
@@ -1966,9 +1842,7 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
             }
             __builtin_amdgcn_s_sleep(2);
         }
-#if BMQCRC_PLAN_DIAG != 5
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
         if (lane == 0) {
             go = ok;
         }
@@ -1979,14 +1853,6 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
         deferred();
         return;
     }
-#if BMQCRC_PLAN_DIAG == 2
-    // diagnostic (timing only): phase 1 and the wait, no map
-    if (threadIdx.x == 0) {
-        __hip_atomic_store(&sync[2], (unsigned long long)ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    deferred();
-    return;
-#endif
     // Batch shape and size from every block's words: closed-form batches and
     // those past seginfo's capacity (or 32-bit indices) need no map.
     // Every load of the other blocks' words goes out at once: the block
@@ -2034,19 +1900,12 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
             map = all <= min((unsigned long long)a.max_segs, (unsigned long long)kSegLimit);
         }
     }
+    // seg_first is written even with the map: another block may have given
+    // the map up after this one saw every arrival (its timer ran out between
+    // two polls), and then k_fold searches seg_first for every block.
+    deferred();
     if (!map) {
-        deferred();
         return;
-    }
-    // With the map k_fold never reads seg_first: only out[] is initialised.
-    {
-        const bool keep_sf = BMQCRC_PLAN_DIAG >= 4;  // diag 4, 5 void the map below
-#pragma unroll
-        for (uint32_t t = 0; t < kMapRegTiles; ++t) {
-            if (t < ntiles) {
-                tile_words(lo + (uint64_t)t * kTile, Lr[t], R0[t], keep_sf);
-            }
-        }
     }
     // This block's slice of every class (k_plan_sort's bucket-major order).
     {
@@ -2108,7 +1967,7 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
                 pos = atomicAdd(&run[c_full], tf);
             }
             pos = (uint32_t)__shfl((int)pos, 0) + (x - nf_all);
-#if BMQCRC_PLAN_DIAG < 4
+#if BMQCRC_PLAN_DIAG != 4
             uint32_t at = pos;
 #pragma unroll
             for (uint32_t v = 0; v < kPlanV; ++v) {
@@ -2151,7 +2010,7 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
             if (c < (uint32_t)kBuckets) {
                 const uint64_t i = base + (uint64_t)threadIdx.x * kPlanV + v;
                 const uint32_t at = atomicAdd(&run[c], 1u);
-#if BMQCRC_PLAN_DIAG < 4
+#if BMQCRC_PLAN_DIAG != 4
                 put_last(a, at, (uint32_t)i);
 #else
                 (void)at;
@@ -2181,8 +2040,8 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
     }
     __syncthreads();
     PLAN_STAMP(3)
-#if BMQCRC_PLAN_DIAG >= 4
-    // diagnostic (timing only): no seginfo stores, so no map; seg_first written
+#if BMQCRC_PLAN_DIAG == 4
+    // diagnostic (timing only): no seginfo stores, so no map
     if (threadIdx.x == 0) {
         __hip_atomic_store(&sync[2], (unsigned long long)ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }

@@ -193,7 +193,8 @@ int bmqcrc_forget_shape(int device, void* stream);
  * leaves, and the fold then maps segments by binary search -- results are
  * exact either way, only slower.  0 gives every map up at once (a test hook
  * for that path).  *voided (may be NULL) receives how many planned batches on
- * (device, stream) gave up their map so far (read after the stream is idle). */
+ * (device, stream) gave up their map so far; asking for it waits for the
+ * work already enqueued on that stream. */
 int bmqcrc_plan_wait(int device, void* stream, uint64_t wait_us, uint64_t* voided);
 
 /* Zero-copy input: page-lock `bytes` of ordinary host memory at `host` and map

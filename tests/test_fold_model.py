@@ -375,41 +375,6 @@ def test_move_byte_tables_match_xpow():
         assert G.mulmod_r(moved, f) == raw
 
 
-def _table_step(ty, c, r0, r1):
-    """k_fold's horner_step with the header's slicing tables."""
-    v = c ^ r0
-    return (ty[4][v & 255] ^ ty[5][(v >> 8) & 255] ^ ty[6][(v >> 16) & 255] ^ ty[7][v >> 24] ^
-            ty[0][r1 & 255] ^ ty[1][(r1 >> 8) & 255] ^ ty[2][(r1 >> 16) & 255] ^ ty[3][r1 >> 24])
-
-
-def test_two_chain_remainder_matches_horner():
-    """tail_horner2 (round 3): words 0..15 and 16..31 reduced as two chains,
-    raw = c_a * y^16 + c_b with the TY16 tables, equals the one-chain Horner
-    and the model's word-by-word reduction."""
-    flat = _header_table("BMQCRC_TY")
-    ty = [flat[256 * k:256 * (k + 1)] for k in range(8)]
-    f16 = _header_table("BMQCRC_TY16")
-    assert len(f16) == 4 * 256
-    t16 = [f16[256 * k:256 * (k + 1)] for k in range(4)]
-    rng = np.random.default_rng(5)
-    for trial in range(200):
-        R = [int(w) for w in rng.integers(0, 2**32, size=32, dtype=np.uint64)]
-        if trial % 3 == 0:
-            R[:16] = [0] * 16  # the one-line skip case: c_a = 0
-        one = 0
-        for d in range(0, 32, 2):
-            one = _table_step(ty, one, R[d], R[d + 1])
-        ca = cb = 0
-        for d in range(0, 16, 2):
-            ca = _table_step(ty, ca, R[d], R[d + 1])
-            cb = _table_step(ty, cb, R[16 + d], R[17 + d])
-        two = cb ^ t16[0][ca & 255] ^ t16[1][(ca >> 8) & 255] ^ t16[2][(ca >> 16) & 255] ^ \
-            t16[3][ca >> 24]
-        assert one == two == horner_words(R)
-        if trial % 3 == 0:
-            assert cb == one  # tail_horner2<8>
-
-
 def _decode_groups(entries, firstk):
     """k_fold's resolve_sorted over every group of 64 entries."""
     LAST = 0x80000000
