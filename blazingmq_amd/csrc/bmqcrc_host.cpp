@@ -217,18 +217,15 @@ uint64_t max_segs_for(uint64_t n, uint64_t arena_bytes, uint32_t seg)
     return n + arena_bytes / seg + 64;
 }
 
-// Contiguous ranges of whole kPlanBlock tiles, at most kPlanMaxBlocks blocks
-// (and at least kPlanMinTiles tiles per block while that leaves >= 32 blocks).
-#ifndef BMQCRC_PLAN_MIN_TILES
-#define BMQCRC_PLAN_MIN_TILES 1
-#endif
-constexpr uint64_t kPlanMinTiles = BMQCRC_PLAN_MIN_TILES;
-
+// Contiguous ranges of whole kPlanBlock tiles, at most kPlanMaxBlocks blocks.
+// (As many blocks as possible: the planners are latency-bound per block.
+// Fewer, fuller blocks -- at least 8 tiles each, so that the 1/8 Zipf shard
+// takes the single-pass planner -- traced 36.8 against 26.3 us there,
+// profiles/r03/ab/planner_block_sizing/.)
 static void split_ranges(uint64_t items, uint64_t* per, uint32_t* blocks)
 {
     const uint64_t tiles = std::max<uint64_t>((items + kPlanBlock - 1) / kPlanBlock, 1);
-    const uint64_t min_tiles = std::min<uint64_t>(kPlanMinTiles, std::max<uint64_t>(tiles / 32, 1));
-    const uint64_t nb = std::min<uint64_t>((tiles + min_tiles - 1) / min_tiles, kPlanMaxBlocks);
+    const uint64_t nb = std::min<uint64_t>(tiles, kPlanMaxBlocks);
     const uint64_t tiles_per = (tiles + nb - 1) / nb;
     *per = tiles_per * kPlanBlock;
     *blocks = (uint32_t)((tiles + tiles_per - 1) / tiles_per);
