@@ -59,6 +59,43 @@ def test_fuzz_batch(cuda, round_):
     assert bad.size == 0, (round_, n, seg, whole, bad[:5], lens[bad[:5]], offs[bad[:5]])
 
 
+@pytest.mark.parametrize("round_", range(max(2, ROUNDS // 8)))
+def test_fuzz_single_pass_planner(cuda, round_):
+    # Batches of more than four planner tiles per block (> 1.3M messages) are
+    # planned by k_plan_map (round 3): random length mixes, overlapping
+    # unaligned offsets, random seeds and segment sizes, a random wait limit
+    # (0 gives the size-class map up), twice in a row on one stream.
+    import torch
+    from blazingmq_amd import last_launch, plan_wait
+    rng = np.random.default_rng(5000 + round_)
+    n = int(rng.integers(1_350_000, 1_800_000))
+    parts = [rng.integers(0, 300, size=n - n // 64)]
+    parts.append(np.minimum(_lengths(rng, n // 64), 65536))
+    lens = np.concatenate(parts).astype(np.uint32)
+    rng.shuffle(lens)
+    arena_size = int(lens.max(initial=0)) + (48 << 20)
+    arena = rng.integers(0, 256, size=arena_size, dtype=np.uint8)
+    offs = (rng.random(n) * (arena_size - lens.astype(np.int64) + 1)).astype(np.uint64)
+    seeds = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32) \
+        if rng.integers(0, 2) else None
+    seg = int(rng.choice([0, 0, 256, 1024, 2048, 16384]))
+    exp = oracle.batch(arena, offs, lens, seeds, nthreads=8)
+    a = torch.from_numpy(arena).to(cuda)
+    o = torch.from_numpy(offs.astype(np.int64)).to(cuda)
+    ln = torch.from_numpy(lens.view(np.int32)).to(cuda)
+    sd = None if seeds is None else torch.from_numpy(seeds.view(np.int32)).to(cuda)
+    s = torch.cuda.Stream(cuda)
+    s.wait_stream(torch.cuda.current_stream(cuda))
+    plan_wait(cuda.index, s, int(rng.choice([0, 1000])))
+    for _ in range(2):
+        got = Crc32c.calculate_batch(a, o, ln, sd, seg_bytes=seg, stream=s)
+        got = got.cpu().numpy().view(np.uint32)
+        bad = np.nonzero(got != exp)[0]
+        assert bad.size == 0, (round_, n, seg, bad[:5], lens[bad[:5]], offs[bad[:5]])
+        assert last_launch(cuda.index, s)["kernels"] == 2  # k_plan_map + k_fold
+    plan_wait(cuda.index, s, 1000)
+
+
 @pytest.mark.parametrize("round_", range(max(4, ROUNDS // 4)))
 def test_fuzz_gather(cuda, round_):
     """bmqcrc_crc32c_gather on random Blob-shaped batches: buffer sizes from
