@@ -27,7 +27,8 @@ constexpr int kBuckets = 16;            // segment size classes: floor(log2(line
 // forces 2, bit4 always builds the size-class map (no shape prediction),
 // bit5 reads one- and two-line groups non-temporally too, bit7 plans ragged
 // batches with the round-2 pair k_plan<true> + k_plan_sort instead of the
-// single-pass k_plan_map.
+// single-pass k_plan_map, bit9 plans them with k_plan_map even when its
+// blocks hold a single tile.
 #ifndef BMQCRC_TUNE_BITS
 #define BMQCRC_TUNE_BITS 0u
 #endif
@@ -102,7 +103,7 @@ constexpr uint32_t kSegLast = 0x80000000u;  // seginfo: the entry is its message
 // (TUNE bit 7 forces the pair).
 inline bool single_pass_planner(const BatchArgs& a)
 {
-    return a.per_msg > (uint64_t)kPlanBlock * kPlanV && !(a.tune & 128u);
+    return (a.per_msg > (uint64_t)kPlanBlock * kPlanV || (a.tune & 512u)) && !(a.tune & 128u);
 }
 
 constexpr uint32_t kHintUnknown = 0;

@@ -51,6 +51,10 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const u32x4 lds_cu4;
 typedef __attribute__((address_space(3))) u32x4 lds_u4;
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+// element-aligned vectors: one dwordx4 access at any dword-aligned address
+typedef uint32_t u32x4e __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint64_t u64x2e __attribute__((ext_vector_type(2), aligned(8)));
 
 __constant__ uint32_t c_x2col[31][32] = BMQCRC_X2COL;
 __constant__ uint32_t c_xneg8[136] = BMQCRC_XNEG8;
@@ -172,6 +176,55 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v)
     v = dpp_max<0x118, 0xf>(v);  // row_shr:8
     v = dpp_max<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
     v = dpp_max<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+// Inclusive prefix sum over the wave's 64 lanes by DPP (all lanes active):
+// row_shr 1/2/4/8 scan each row of 16, row_bcast 15/31 carry the row totals.
+// Lanes without a source add old = 0.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_add(uint32_t v)
+{
+    return v + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xf, false);
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
+{
+    v = dpp_add<0x111, 0xf>(v);  // row_shr:1
+    v = dpp_add<0x112, 0xf>(v);  // row_shr:2
+    v = dpp_add<0x114, 0xf>(v);  // row_shr:4
+    v = dpp_add<0x118, 0xf>(v);  // row_shr:8
+    v = dpp_add<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
+    v = dpp_add<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(v), 63);
+}
+
+// 64-bit wave sum of per-lane values below 2^38 (two 32-bit scans)
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v)
+{
+    return ((uint64_t)wave_sum((uint32_t)(v >> 16)) << 16) + wave_sum((uint32_t)v & 0xffffu);
+}
+
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_min(uint32_t v)
+{
+    return min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, ROW_MASK, 0xf,
+                                                        false));
+}
+
+__device__ __forceinline__ uint32_t wave_min(uint32_t v)
+{
+    v = dpp_min<0x111, 0xf>(v);
+    v = dpp_min<0x112, 0xf>(v);
+    v = dpp_min<0x114, 0xf>(v);
+    v = dpp_min<0x118, 0xf>(v);
+    v = dpp_min<0x142, 0xa>(v);
+    v = dpp_min<0x143, 0xc>(v);
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
@@ -499,29 +552,22 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* excl, uint3
 {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nw = blockDim.x >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
-        if (lane >= o) {
-            x += y;
-        }
-    }
+    const uint32_t x = wave_incl_scan(v);
     if (lane == 63) {
         wsum[wave] = x;
     }
     __syncthreads();
-    if (threadIdx.x < 16) {
-        uint32_t w = (int)threadIdx.x < nw ? wsum[threadIdx.x] : 0u, y = w;
-        for (int o = 1; o < 16; o <<= 1) {
-            const uint32_t z = (uint32_t)__shfl_up((int)y, o, 16);
-            if ((int)threadIdx.x >= o) {
-                y += z;
+    if (threadIdx.x < 64) {  // wave 0 (DPP needs whole rows): row 0 scans the wave totals
+        const uint32_t w = (int)threadIdx.x < nw ? wsum[threadIdx.x] : 0u;
+        uint32_t y = dpp_add<0x111, 0xf>(w);  // row_shr:1
+        y = dpp_add<0x112, 0xf>(y);           // row_shr:2
+        y = dpp_add<0x114, 0xf>(y);           // row_shr:4
+        y = dpp_add<0x118, 0xf>(y);           // row_shr:8
+        if (threadIdx.x < 16) {
+            wsum[16 + threadIdx.x] = y - w;  // exclusive wave prefix
+            if (threadIdx.x == 15) {
+                wsum[32] = y;
             }
-        }
-        wsum[16 + threadIdx.x] = y - w;  // exclusive wave prefix
-        if (threadIdx.x == 15) {
-            wsum[32] = y;
         }
     }
     __syncthreads();
@@ -1243,6 +1289,113 @@ __device__ __forceinline__ uint32_t msg_segments(const BatchArgs& a, uint64_t of
     return nseg;
 }
 
+// Lengths and offsets of messages i0 .. i0 + kPlanV - 1: one planner
+// thread's quad of a tile.  A whole quad inside [lo, hi) is one dwordx4 load
+// of lengths and two of offsets (the dword form, lanes 16 bytes apart, issued
+// 4x the requests); any other quad loads zeros from g_zero_line, and the
+// batch's last, partial quad (hi = n, n % 4 != 0) is patched from LDS where
+// it is used (PlanTail).  No branch around the loads: a quad assembled in a
+// branch made the compiler copy registers at the join, which waited for the
+// loads there and serialized a block's tiles (phase 1 at ~4 us per tile,
+// profiles/r03/ab/planner_stamps/).
+struct Quad {
+    u32x4 l;
+    u64x2 o0, o1;
+};
+
+struct PlanTail {  // LDS: the last 1-3 messages of the batch, in the block that owns them
+    uint64_t off[kPlanV - 1];
+    uint32_t len[kPlanV - 1];
+};
+
+__device__ __forceinline__ Quad load_quad(const BatchArgs& a, uint64_t i0, uint64_t hi,
+                                          bool offsets = true)
+{
+    static_assert(kPlanV == 4, "quad loads");
+    const bool whole = i0 + kPlanV <= hi;
+    const uint32_t* lp = whole ? a.lengths + i0 : (const uint32_t*)g_zero_line;
+    const uint64_t* op = (whole && offsets) ? a.offsets + i0 : (const uint64_t*)g_zero_line;
+    Quad q;
+    q.l = *(const u32x4e*)lp;
+    q.o0 = *(const u64x2e*)op;
+    q.o1 = *(const u64x2e*)(op + 2);
+    return q;
+}
+
+// Thread 0 of the block whose range ends the batch with a partial quad
+// (before the block's first barrier).
+__device__ __forceinline__ void load_tail(const BatchArgs& a, uint64_t hi, bool offsets,
+                                          PlanTail* t)
+{
+    if (threadIdx.x == 0 && hi == a.n && (hi & 3u)) {
+        const uint64_t i0 = hi & ~3ull;
+        for (uint32_t v = 0; v < (uint32_t)(hi & 3u); ++v) {
+            t->len[v] = a.lengths[i0 + v];
+            t->off[v] = offsets ? a.offsets[i0 + v] : 0ull;
+        }
+    }
+}
+
+__device__ __forceinline__ void unpack_quad(const Quad& q, uint64_t i0, uint64_t hi,
+                                            const PlanTail* t, uint32_t (&L)[kPlanV],
+                                            uint64_t (&O)[kPlanV])
+{
+    L[0] = q.l.x;
+    L[1] = q.l.y;
+    L[2] = q.l.z;
+    L[3] = q.l.w;
+    O[0] = q.o0.x;
+    O[1] = q.o0.y;
+    O[2] = q.o1.x;
+    O[3] = q.o1.y;
+    if (i0 < hi && i0 + kPlanV > hi) {  // the batch's partial last quad
+#pragma unroll
+        for (uint32_t v = 0; v < kPlanV - 1; ++v) {
+            if (i0 + v < hi) {
+                L[v] = t->len[v];
+                O[v] = t->off[v];
+            }
+        }
+    }
+}
+
+// seg_first (exclusive prefix from r) and out[] initialisation of one
+// planner thread's quad: one dwordx4 store each for a whole quad.  out gets
+// 0 for every non-empty message (a one-segment message is stored whole by
+// its lane in k_fold, later on the stream; others XOR-accumulate from 0) and
+// the seed for an empty one.
+__device__ __forceinline__ void store_quad(const BatchArgs& a, uint64_t i0, uint64_t hi,
+                                           const uint32_t (&L)[kPlanV], const uint32_t (&ns)[kPlanV],
+                                           uint32_t r, bool write_sf)
+{
+    uint32_t sf[kPlanV], o[kPlanV];
+#pragma unroll
+    for (uint32_t v = 0; v < kPlanV; ++v) {
+        sf[v] = r;
+        r += ns[v];
+        o[v] = 0u;
+        if (L[v] == 0u && a.seeds && i0 + v < hi) {
+            o[v] = a.seeds[i0 + v];
+        }
+    }
+    if (i0 + kPlanV <= hi) {
+        if (write_sf) {
+            *(u32x4e*)(a.seg_first + i0) = u32x4{sf[0], sf[1], sf[2], sf[3]};
+        }
+        *(u32x4e*)(a.out + i0) = u32x4{o[0], o[1], o[2], o[3]};
+        return;
+    }
+#pragma unroll
+    for (uint32_t v = 0; v < kPlanV; ++v) {
+        if (i0 + v < hi) {
+            if (write_sf) {
+                a.seg_first[i0 + v] = sf[v];
+            }
+            a.out[i0 + v] = o[v];
+        }
+    }
+}
+
 // K1: segment counts per message, the block-local exclusive prefix over the
 // block's contiguous message range (seg_first), out[] initialisation, and
 // three words per block (segments, messages with != 1 segment, the common
@@ -1258,7 +1411,9 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
     __shared__ uint32_t sh[4];
     __shared__ uint32_t hist[kBuckets];
     __shared__ unsigned long long segs64;  // the block's segments without wrapping
+    __shared__ PlanTail tail;
     constexpr bool classes = CLASSES;  // a ragged batch is expected: size-class histogram
+    load_tail(a, min((uint64_t)blockIdx.x * a.per_msg + a.per_msg, a.n), classes, &tail);
     if (threadIdx.x == 0) {
         sh[1] = 0;            // messages with != 1 segment
         sh[2] = 0xffffffffu;  // min segments per message
@@ -1269,24 +1424,17 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
         hist[threadIdx.x] = 0;
     }
     __syncthreads();
-    const int lane = threadIdx.x & 63;
     constexpr uint64_t kTile = (uint64_t)kPlanBlock * kPlanV;
     const uint64_t lo = (uint64_t)blockIdx.x * a.per_msg;
     const uint64_t hi = min(lo + a.per_msg, a.n);
     const uint32_t seg = a.seg_bytes;
     const uint32_t seg_shift = (seg & (seg - 1u)) == 0 ? (uint32_t)__builtin_ctz(seg) : 0u;
-    auto load = [&](uint64_t base, uint32_t (&L)[kPlanV], uint64_t (&O)[kPlanV]) {
-#pragma unroll
-        for (uint32_t v = 0; v < kPlanV; ++v) {
-            const uint64_t i = base + (uint64_t)threadIdx.x * kPlanV + v;
-            L[v] = i < hi ? a.lengths[i] : 0u;
-            O[v] = (classes && i < hi) ? a.offsets[i] : 0ull;
-        }
+    auto load = [&](uint64_t base) {
+        return load_quad(a, base + (uint64_t)threadIdx.x * kPlanV, hi, classes);
     };
-    uint32_t nxt[kPlanV];
-    uint64_t nxo[kPlanV];
+    Quad nq;
     if (lo < hi) {
-        load(lo, nxt, nxo);
+        nq = load(lo);
     }
     uint32_t full = 0;  // this thread's non-last segments (all of class c_full)
     // A single-tile block (<= 4096 messages: every batch of <= 1M messages)
@@ -1299,13 +1447,9 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
     for (uint64_t base = lo; base < hi; base += kTile) {
         uint32_t L[kPlanV];
         uint64_t O[kPlanV];
-#pragma unroll
-        for (uint32_t v = 0; v < kPlanV; ++v) {
-            L[v] = nxt[v];
-            O[v] = nxo[v];
-        }
+        unpack_quad(nq, base + (uint64_t)threadIdx.x * kPlanV, hi, &tail, L, O);
         if (base + kTile < hi) {
-            load(base + kTile, nxt, nxo);  // next tile in flight during this scan
+            nq = load(base + kTile);  // next tile in flight during this scan
         }
         if (classes) {
             // class of each message's last (or only) segment: one
@@ -1328,11 +1472,6 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
             const uint32_t len = L[v];
             ns[v] = len ? (seg_shift ? ((len - 1u) >> seg_shift) : (len - 1u) / seg) + 1u : 0u;
             if (i < hi) {
-                // a one-segment message is stored whole by its lane in k_fold;
-                // others XOR-accumulate (from 0) or keep the seed (empty)
-                if (ns[v] != 1u) {
-                    a.out[i] = len ? 0u : (a.seeds ? a.seeds[i] : 0u);
-                }
                 mn = min(mn, ns[v]);
                 mx = max(mx, ns[v]);
                 non1 += ns[v] != 1u ? 1u : 0u;
@@ -1343,36 +1482,19 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
         uint32_t excl;
         const uint32_t tot = block_scan(sum, &excl, wsum);
         run0 = carry + excl;
-        if (!one_tile) {
-            uint32_t run = run0;
-#pragma unroll
-            for (uint32_t v = 0; v < kPlanV; ++v) {
-                const uint64_t i = base + (uint64_t)threadIdx.x * kPlanV + v;
-                if (i < hi) {
-                    a.seg_first[i] = run;
-                }
-                run += ns[v];
-            }
-        }
+        // seg_first (multi-tile blocks; a single tile's waits for the block's
+        // shape below) and out[]
+        store_quad(a, base + (uint64_t)threadIdx.x * kPlanV, hi, L, ns, run0, !one_tile);
         carry += tot;
     }
     // block-level min / max / count(!=1): wave reductions, then LDS atomics
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
-        mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
-        non1 += (uint32_t)__shfl_xor((int)non1, o);
-    }
+    mn = wave_min(mn);
+    mx = wave_max(mx);
+    non1 = wave_sum(non1);
     if (classes) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            full += (uint32_t)__shfl_xor((int)full, o);
-        }
+        full = wave_sum(full);
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        mine64 += shfl64(mine64, lane ^ o);
-    }
+    mine64 = wave_sum64(mine64);
     if ((threadIdx.x & 63) == 0) {
         atomicMin(&sh[2], mn);
         atomicMax(&sh[3], mx);
@@ -1387,14 +1509,22 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan(BatchArgs a)
         a.bhist[(uint64_t)blockIdx.x * kBuckets + threadIdx.x] = hist[threadIdx.x];
     }
     if (one_tile && sh[2] != sh[3]) {
-        uint32_t run = run0;
+        uint32_t sf[kPlanV], run = run0;
 #pragma unroll
         for (uint32_t v = 0; v < kPlanV; ++v) {
-            const uint64_t i = lo + (uint64_t)threadIdx.x * kPlanV + v;
-            if (i < hi) {
-                a.seg_first[i] = run;
-            }
+            sf[v] = run;
             run += ns[v];
+        }
+        const uint64_t i0 = lo + (uint64_t)threadIdx.x * kPlanV;
+        if (i0 + kPlanV <= hi) {
+            *(u32x4e*)(a.seg_first + i0) = u32x4{sf[0], sf[1], sf[2], sf[3]};
+        } else {
+#pragma unroll
+            for (uint32_t v = 0; v < kPlanV; ++v) {
+                if (i0 + v < hi) {
+                    a.seg_first[i0 + v] = sf[v];
+                }
+            }
         }
     }
     if (threadIdx.x == 0) {  // read by the next launches (kernel boundary: plain stores)
@@ -1456,6 +1586,7 @@ __device__ __forceinline__ void put_last(const BatchArgs& a, uint32_t pos, uint3
 // 61.5 us with every run walked by the wave, 52 with 4-segment short runs,
 // 49.5 with 8, 51.4 with 16 (same-box A/B, profiles/r02/ab/).
 constexpr uint32_t kShortRun = 8u;
+constexpr uint32_t kMapShortRun = 16u;  // k_plan_map: runs the wave writes through its search
 
 __global__ __launch_bounds__(kPlanBlock) void k_plan_sort(BatchArgs a)
 {
@@ -1593,8 +1724,9 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_sort(BatchArgs a)
 // The blocks then meet once, grid-wide; after that every block reads all
 // histograms and writes the rest: (message, k) of its segments into its
 // slice of every class -- exactly k_plan_sort's global class-major order --
-// plus seg_first and the out[] initialisation, which phase 1 defers so that
-// the arrival's L2 write-back carries only the block words.  (A block-major
+// plus seg_first and the out[] initialisation, which phase 1 defers (they
+// are not needed before the wait, and the deferred stores are one dwordx4
+// per quad).  (A block-major
 // order -- each block's slice sorted by class, offsets by a decoupled
 // look-back, no grid-wide wait -- was measured first: k_fold's grid-stride
 // waves then draw a binomial mix of 16-round and 1-round groups, and Zipf's
@@ -1612,6 +1744,11 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_sort(BatchArgs a)
 #define BMQCRC_MAP_REG_TILES 4
 #endif
 constexpr uint32_t kMapRegTiles = BMQCRC_MAP_REG_TILES;  // tiles kept in registers across the wait
+#ifndef BMQCRC_PLAN_SKIP
+#define BMQCRC_PLAN_SKIP 0  // timing diagnostics with the map voided (wrong maps, exact CRCs):
+                            // 1 no histogram atomics, 2 no last-segment claims, 4 no full-run
+                            // writes, 8 no last-segment stores
+#endif
 #ifndef BMQCRC_PLAN_DIAG
 #define BMQCRC_PLAN_DIAG 0  // 3: per-block phase stamps, 4: the same without seginfo stores
                             // (timing diagnostics, tools/plan_trace_diag.py); product: 0
@@ -1619,14 +1756,22 @@ constexpr uint32_t kMapRegTiles = BMQCRC_MAP_REG_TILES;  // tiles kept in regist
 
 #if BMQCRC_PLAN_DIAG >= 3
 // diagnostic build only: per-block wall-clock stamps of the last launch
-// (start, phase 1 done, wait done, end), read by bmqcrc_diag_plan_trace
-__device__ unsigned long long g_plan_trace[kPlanMaxBlocks][4];
+// (start, first loads landed, first tile counted, phase 1 done, wait done,
+// deferred writes issued, class bases done, end), read by
+// bmqcrc_diag_plan_trace
+__device__ unsigned long long g_plan_trace[kPlanMaxBlocks][8];
 #define PLAN_STAMP(k)                                                        \
     if (threadIdx.x == 0) {                                                  \
         g_plan_trace[blockIdx.x][k] = wall_clock64();                        \
     }
+#define PLAN_STAMP_LANDED(k)                                                 \
+    if (threadIdx.x == 0) {                                                  \
+        __builtin_amdgcn_s_waitcnt(0);                                       \
+        g_plan_trace[blockIdx.x][k] = wall_clock64();                        \
+    }
 #else
 #define PLAN_STAMP(k)
+#define PLAN_STAMP_LANDED(k)
 #endif
 
 __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
@@ -1639,7 +1784,10 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
     __shared__ uint32_t part[2][kPlanBlock / kBuckets][kBuckets];
     __shared__ unsigned long long segs64;
     __shared__ uint32_t go;
+    __shared__ PlanTail tail;
+    __shared__ uint32_t sruns[kPlanBlock / 64][64 * kPlanV];  // per wave: short-run ends
     const uint32_t nb = a.nblocks, ep = a.plan_epoch, bid = blockIdx.x;
+    load_tail(a, min((uint64_t)bid * a.per_msg + a.per_msg, a.n), true, &tail);
     unsigned long long* const sync = a.plan_sync;
     if (threadIdx.x == 0) {
         sh[1] = 0;            // messages with != 1 segment
@@ -1665,57 +1813,38 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
     };
 
     // Thread t of tile [base, base + kTile) owns messages base + 4t .. base + 4t + 3.
-    auto load = [&](uint64_t base, uint32_t (&L)[kPlanV], uint64_t (&O)[kPlanV]) {
-#pragma unroll
-        for (uint32_t v = 0; v < kPlanV; ++v) {
-            const uint64_t i = base + (uint64_t)threadIdx.x * kPlanV + v;
-            L[v] = i < hi ? a.lengths[i] : 0u;
-            O[v] = i < hi ? a.offsets[i] : 0ull;
-        }
+    auto load = [&](uint32_t t) {
+        return load_quad(a, lo + (uint64_t)t * kTile + (uint64_t)threadIdx.x * kPlanV, hi);
     };
     // seg_first (the block-local prefix from run0) and out[] for one tile
     auto tile_words = [&](uint64_t base, const uint32_t (&L)[kPlanV], uint32_t run0,
                           bool write_sf) {
-        uint32_t r = run0;
+        uint32_t ns[kPlanV];
 #pragma unroll
         for (uint32_t v = 0; v < kPlanV; ++v) {
-            const uint64_t i = base + (uint64_t)threadIdx.x * kPlanV + v;
-            const uint32_t ns = segments(L[v]);
-            if (i < hi) {
-                if (write_sf) {
-                    a.seg_first[i] = r;
-                }
-                if (ns != 1u) {  // XOR-accumulated in k_fold (from 0; empty: the seed)
-                    a.out[i] = L[v] ? 0u : (a.seeds ? a.seeds[i] : 0u);
-                }
-            }
-            r += ns;
+            ns[v] = segments(L[v]);
         }
+        store_quad(a, base + (uint64_t)threadIdx.x * kPlanV, hi, L, ns, run0, write_sf);
     };
-    // Phase 1, per tile (the next tile's loads in flight meanwhile).  The
-    // first kMapRegTiles tiles keep their lengths, classes and prefix in
-    // registers and defer their writes; later tiles write as k_plan does.
+    // Phase 1.  The first kMapRegTiles tiles are loaded at once (all in
+    // flight together) and keep their lengths, classes and prefix in
+    // registers, deferring their writes; later tiles load one ahead and
+    // write as k_plan does.
     uint32_t Lr[kMapRegTiles][kPlanV], Cr[kMapRegTiles], R0[kMapRegTiles];
     uint32_t full = 0, carry = 0, mn = 0xffffffffu, mx = 0, non1 = 0;
     uint64_t mine64 = 0;
-    uint32_t nxt[kPlanV];
-    uint64_t nxo[kPlanV];
-    if (ntiles) {
-        load(lo, nxt, nxo);
+    Quad rq[kMapRegTiles];
+#pragma unroll
+    for (uint32_t t = 0; t < kMapRegTiles; ++t) {
+        rq[t] = load(t);  // unguarded: a tile past the range loads the zero line
     }
-    // (all register tiles loaded up front measured slower: 18.7 -> 22.8 us
-    // for phase 1 on Zipf, profiles/r03/ab/planner_phase_stamps.jsonl)
-    auto count_tile = [&](uint32_t t, uint32_t (&L)[kPlanV], uint32_t& cls, uint32_t& run0,
-                          bool defer) {
+    auto count_tile = [&](uint32_t t, const Quad& q, uint32_t (&L)[kPlanV], uint32_t& cls,
+                          uint32_t& run0, bool defer) {
         const uint64_t base = lo + (uint64_t)t * kTile;
         uint64_t O[kPlanV];
-#pragma unroll
-        for (uint32_t v = 0; v < kPlanV; ++v) {
-            L[v] = nxt[v];
-            O[v] = nxo[v];
-        }
-        if (t + 1u < ntiles) {
-            load(base + kTile, nxt, nxo);  // the next tile in flight during this one
+        unpack_quad(q, base + (uint64_t)threadIdx.x * kPlanV, hi, &tail, L, O);
+        if (t == 0) {
+            PLAN_STAMP_LANDED(1)
         }
         cls = 0;
         uint32_t sum = 0;
@@ -1724,7 +1853,7 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
             uint32_t c;
             const uint32_t ns = msg_segments(a, O[v], L[v], seg_shift, &c);
             full += ns ? ns - 1u : 0u;
-            if (c < (uint32_t)kBuckets) {
+            if (c < (uint32_t)kBuckets && !(BMQCRC_PLAN_SKIP & 1)) {
                 atomicAdd(&hist[c], 1u);
             }
             cls |= c << (8u * v);  // kBuckets (no segment) fits a byte
@@ -1744,28 +1873,34 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
         if (!defer) {
             tile_words(base, L, run0, true);
         }
+        if (t == 0) {
+            PLAN_STAMP(2)
+        }
     };
 #pragma unroll
     for (uint32_t t = 0; t < kMapRegTiles; ++t) {
         if (t < ntiles) {
-            count_tile(t, Lr[t], Cr[t], R0[t], true);
+            count_tile(t, rq[t], Lr[t], Cr[t], R0[t], true);
         }
     }
-    for (uint32_t t = kMapRegTiles; t < ntiles; ++t) {
-        uint32_t L[kPlanV], c, r0;
-        count_tile(t, L, c, r0, false);
+    if (ntiles > kMapRegTiles) {
+        Quad nq = load(kMapRegTiles);
+        for (uint32_t t = kMapRegTiles; t < ntiles; ++t) {
+            const Quad q = nq;
+            if (t + 1u < ntiles) {
+                nq = load(t + 1u);  // the next tile in flight during this one
+            }
+            uint32_t L[kPlanV], c, r0;
+            count_tile(t, q, L, c, r0, false);
+        }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
-        mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
-        non1 += (uint32_t)__shfl_xor((int)non1, o);
-        full += (uint32_t)__shfl_xor((int)full, o);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        mine64 += shfl64(mine64, lane ^ o);
-    }
+    // wave reductions by DPP (the bpermute butterflies were a 6-deep chain
+    // of LDS round trips per value)
+    mn = wave_min(mn);
+    mx = wave_max(mx);
+    non1 = wave_sum(non1);
+    full = wave_sum(full);
+    mine64 = wave_sum64(mine64);
     if ((threadIdx.x & 63) == 0) {
         atomicMin(&sh[2], mn);
         atomicMax(&sh[3], mx);
@@ -1789,26 +1924,34 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
         }
     };
     // Publish the block words and the histogram, then arrive and wait.
-    PLAN_STAMP(1)
-    if (threadIdx.x < kBuckets) {
-        a.bhist[(uint64_t)bid * kBuckets + threadIdx.x] = hist[threadIdx.x];
-    }
-    if (threadIdx.x == 0) {
-        a.block_sum[bid] = segs64 > kSegLimit ? 0xffffffffu : carry;
-        a.block_sum[nb + bid] = sh[1];
-        a.block_sum[2u * nb + bid] = sh[2] == sh[3] ? sh[2] : 0xffffffffu;
-    }
-    __syncthreads();
+    PLAN_STAMP(3)
     if (threadIdx.x < 64) {
-        // Arrival: one flag word per block, set to this launch's epoch (a
-        // release store: the block's words above are visible before it, on
-        // every XCD).  No shared counter -- 256 atomics on one word serialize
-        // at the memory side (11-16 us measured,
-        // profiles/r03/ab/planner_phases_counter_wait/) -- and no reset: a
-        // flag of an older launch holds an older epoch.  Wave 0 polls every
-        // block's flag (relaxed loads; one acquire after).
+        // Wave 0 publishes the block words and the histogram with
+        // device-scope stores (they write through to memory, visible on
+        // every XCD once complete), waits for them, then arrives: one flag
+        // word per block, set to this launch's epoch.  The readers load all
+        // of it with device-scope loads, so neither side needs an agent-scope
+        // fence (an L2 write-back / invalidate: ~3 us of the wait,
+        // profiles/r03/ab/planner_stamps/).  No shared counter -- 256
+        // atomics on one word serialize at the memory side (11-16 us
+        // measured, profiles/r03/ab/planner_phases_counter_wait/) -- and no
+        // reset: a flag of an older launch holds an older epoch.
+        if (lane < kBuckets) {
+            __hip_atomic_store(&a.bhist[(uint64_t)bid * kBuckets + lane], hist[lane],
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         if (lane == 0) {
-            __hip_atomic_store(&sync[kSyncFlags + bid], (unsigned long long)ep, __ATOMIC_RELEASE,
+            __hip_atomic_store(&a.block_sum[bid], segs64 > kSegLimit ? 0xffffffffu : carry,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&a.block_sum[nb + bid], sh[1], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&a.block_sum[2u * nb + bid], sh[2] == sh[3] ? sh[2] : 0xffffffffu,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __builtin_amdgcn_s_waitcnt(0);  // the stores above are complete (vmcnt 0)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) {
+            __hip_atomic_store(&sync[kSyncFlags + bid], (unsigned long long)ep, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
         const uint64_t t0 = wall_clock64();
@@ -1842,13 +1985,13 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
             }
             __builtin_amdgcn_s_sleep(2);
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         if (lane == 0) {
             go = ok;
         }
     }
     __syncthreads();
-    PLAN_STAMP(2)
+    PLAN_STAMP(4)
     if (!go) {
         deferred();
         return;
@@ -1867,26 +2010,29 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
 #pragma unroll
         for (uint32_t k = 0; k < 4; ++k) {
             const uint32_t b = pi + kParts * k;
-            hb[k] = b < nb ? a.bhist[(uint64_t)b * kBuckets + c] : 0u;
+            hb[k] = b < nb ? __hip_atomic_load(&a.bhist[(uint64_t)b * kBuckets + c],
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                           : 0u;
         }
     }
     bool map = true;
     {
         const uint32_t j = threadIdx.x;
-        const uint32_t v = j < nb ? a.block_sum[j] : 0u;
-        const uint32_t nn = j < nb ? a.block_sum[nb + j] : 0u;
-        const uint32_t u0 = a.block_sum[2u * nb];
-        const uint32_t u = j < nb ? a.block_sum[2u * nb + j] : u0;
+        auto word = [&](uint32_t w) {
+            return __hip_atomic_load(&a.block_sum[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        };
+        const uint32_t v = j < nb ? word(j) : 0u;
+        const uint32_t nn = j < nb ? word(nb + j) : 0u;
+        const uint32_t u0 = word(2u * nb);
+        const uint32_t u = j < nb ? word(2u * nb + j) : u0;
         const int ragged = __syncthreads_or(nn != 0u);
         const int mixed = __syncthreads_or(u != u0);
         if (!ragged || (!mixed && u0 != 0xffffffffu)) {
             map = false;  // identity or uniform: k_fold uses closed forms
         } else {
-            unsigned long long sum = v == 0xffffffffu ? (1ull << 40) : v;
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                sum += (unsigned long long)shfl64(sum, lane ^ o);
-            }
+            // (a block over the limit counts as 2^32, past any capacity)
+            const unsigned long long sum =
+                wave_sum64(v) + (v == 0xffffffffu ? 1ull : 0ull);
             if (lane == 0) {
                 wsum[threadIdx.x >> 6] = (uint32_t)min(sum, (unsigned long long)0xffffffffu);
             }
@@ -1904,6 +2050,7 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
     // the map up after this one saw every arrival (its timer ran out between
     // two polls), and then k_fold searches seg_first for every block.
     deferred();
+    PLAN_STAMP(5)
     if (!map) {
         return;
     }
@@ -1938,67 +2085,76 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
         }
         __syncthreads();
     }
+    PLAN_STAMP(6)
     // Phase 2: (message, k) of every segment.
     auto write_tile = [&](uint32_t t, const uint32_t (&L)[kPlanV], uint32_t cls) {
         const uint64_t base = lo + (uint64_t)t * kTile;
-        // Full segments: one claim per wave for all its runs (a wave-wide
-        // exclusive scan of the lanes' counts), so the wave's runs are one
-        // contiguous range, lane by lane.  A lane writes a short run itself;
-        // the wave writes each long run together (coalesced).
-        uint32_t nseg[kPlanV], nf[kPlanV], nf_all = 0;
+        // Full segments: one claim per wave for all its runs, short ones
+        // (at most kMapShortRun segments) first, then long ones; each kind
+        // in (lane, v) order.  The wave writes the short runs' range
+        // together, 64 consecutive entries per store: slot j finds its run
+        // by a binary search over the runs' ends, staged in LDS.  (Each lane
+        // writing its own runs issued up to 4 kShortRun scattered stores per
+        // tile: 16 of the planner's 58 us on Zipf 4M,
+        // profiles/r03/ab/planner_stamps/sk1_component_skips.jsonl.)
+        // Each long run is written by the whole wave, coalesced.
+        uint32_t nf[kPlanV], ns_all = 0, nl_all = 0;
 #pragma unroll
         for (uint32_t v = 0; v < kPlanV; ++v) {
-            nseg[v] = segments(L[v]);
-            nf[v] = nseg[v] ? nseg[v] - 1u : 0u;
-            nf_all += nf[v];
+            const uint32_t nseg = segments(L[v]);
+            nf[v] = nseg ? nseg - 1u : 0u;
+            ns_all += nf[v] <= kMapShortRun ? nf[v] : 0u;
+            nl_all += nf[v] > kMapShortRun ? nf[v] : 0u;
         }
-        uint32_t x = nf_all;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)x, o);
-            if (lane >= o) {
-                x += y;
-            }
-        }
-        const uint32_t tf = (uint32_t)__shfl((int)x, 63);
-        if (tf) {
+        const uint32_t xs = wave_incl_scan(ns_all), xl = wave_incl_scan(nl_all);
+        const uint32_t ts = (uint32_t)__builtin_amdgcn_readlane((int)xs, 63);
+        const uint32_t tl = (uint32_t)__builtin_amdgcn_readlane((int)xl, 63);
+        if (ts + tl) {
             uint32_t pos = 0;
             if (lane == 0) {
-                pos = atomicAdd(&run[c_full], tf);
+                pos = atomicAdd(&run[c_full], ts + tl);
             }
-            pos = (uint32_t)__shfl((int)pos, 0) + (x - nf_all);
-#if BMQCRC_PLAN_DIAG != 4
-            uint32_t at = pos;
+            pos = (uint32_t)__builtin_amdgcn_readfirstlane((int)pos);
+#if BMQCRC_PLAN_DIAG != 4 && !(BMQCRC_PLAN_SKIP & 4)
+            const uint32_t w = threadIdx.x >> 6;
+            const uint64_t wbase = base + (uint64_t)(threadIdx.x & ~63u) * kPlanV;
+            if (ts) {
+                uint32_t e = xs - ns_all, ends[kPlanV];
 #pragma unroll
-            for (uint32_t v = 0; v < kPlanV; ++v) {
-                if (nf[v] <= kShortRun) {
-                    const uint32_t i = (uint32_t)(base + (uint64_t)threadIdx.x * kPlanV + v);
-                    for (uint32_t k = 0; k < nf[v]; ++k) {
-                        put_full(a, at + k, i, k);
-                    }
+                for (uint32_t v = 0; v < kPlanV; ++v) {
+                    e += nf[v] <= kMapShortRun ? nf[v] : 0u;
+                    ends[v] = e;
                 }
-                at += nf[v];
+                *(u32x4*)&sruns[w][lane * kPlanV] = u32x4{ends[0], ends[1], ends[2], ends[3]};
+                for (uint32_t j = (uint32_t)lane; j < ts; j += 64u) {
+                    uint32_t q = 0;  // runs ending at or before j
+#pragma unroll
+                    for (uint32_t st = 32u * kPlanV; st; st >>= 1) {
+                        q += sruns[w][q + st - 1u] <= j ? st : 0u;
+                    }
+                    const uint32_t k = j - (q ? sruns[w][q - 1u] : 0u);
+                    put_full(a, pos + j, (uint32_t)(wbase + q), k);
+                }
             }
-            const uint32_t lane0 = threadIdx.x & ~63u;
             uint64_t longs = 0;
 #pragma unroll
             for (uint32_t v = 0; v < kPlanV; ++v) {
-                longs |= __ballot(nf[v] > kShortRun);
+                longs |= __ballot(nf[v] > kMapShortRun);
             }
+            const uint32_t lpos = pos + ts + (xl - nl_all);
             for (; longs; longs &= longs - 1ull) {
                 const int src = __builtin_ctzll(longs);
-                uint32_t at2 = (uint32_t)__builtin_amdgcn_readlane((int)pos, src);
+                uint32_t at2 = (uint32_t)__builtin_amdgcn_readlane((int)lpos, src);
 #pragma unroll
                 for (uint32_t v = 0; v < kPlanV; ++v) {
                     const uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)nf[v], src);
-                    if (n > kShortRun) {
-                        const uint32_t i =
-                            (uint32_t)(base + (uint64_t)(lane0 + (uint32_t)src) * kPlanV + v);
+                    if (n > kMapShortRun) {
+                        const uint32_t i = (uint32_t)(wbase + (uint32_t)src * kPlanV + v);
                         for (uint32_t k = (uint32_t)lane; k < n; k += 64u) {
                             put_full(a, at2 + k, i, k);
                         }
+                        at2 += n;
                     }
-                    at2 += n;
                 }
             }
 #endif
@@ -2009,8 +2165,12 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
             const uint32_t c = (cls >> (8u * v)) & 0xffu;
             if (c < (uint32_t)kBuckets) {
                 const uint64_t i = base + (uint64_t)threadIdx.x * kPlanV + v;
+#if BMQCRC_PLAN_SKIP & 2
+                const uint32_t at = run[c] + (uint32_t)threadIdx.x * kPlanV + v;
+#else
                 const uint32_t at = atomicAdd(&run[c], 1u);
-#if BMQCRC_PLAN_DIAG != 4
+#endif
+#if BMQCRC_PLAN_DIAG != 4 && !(BMQCRC_PLAN_SKIP & 8)
                 put_last(a, at, (uint32_t)i);
 #else
                 (void)at;
@@ -2028,7 +2188,8 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
     for (uint32_t t = kMapRegTiles; t < ntiles; ++t) {
         uint32_t L[kPlanV];
         uint64_t O[kPlanV];
-        load(lo + (uint64_t)t * kTile, L, O);
+        unpack_quad(load(t), lo + (uint64_t)t * kTile + (uint64_t)threadIdx.x * kPlanV, hi, &tail,
+                    L, O);
         uint32_t cls = 0;
 #pragma unroll
         for (uint32_t v = 0; v < kPlanV; ++v) {
@@ -2039,8 +2200,8 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
         write_tile(t, L, cls);
     }
     __syncthreads();
-    PLAN_STAMP(3)
-#if BMQCRC_PLAN_DIAG == 4
+    PLAN_STAMP(7)
+#if BMQCRC_PLAN_DIAG == 4 || BMQCRC_PLAN_SKIP
     // diagnostic (timing only): no seginfo stores, so no map
     if (threadIdx.x == 0) {
         __hip_atomic_store(&sync[2], (unsigned long long)ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

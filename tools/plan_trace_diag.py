@@ -1,11 +1,11 @@
 #!/usr/bin/env python3
 """Per-block phase times of k_plan_map (GPU box, diagnostic build only).
 
-Needs a library built with -DBMQCRC_PLAN_DIAG=3 (tools/build_variant.sh pd3
+Needs a library built with -DBMQCRC_PLAN_DIAG=3 or 4 (tools/build_variant.sh pd3
 -DBMQCRC_PLAN_DIAG=3), swapped in as libbmqcrc.so by the caller.  Runs the
 Zipf batch (or one shard of it) a few times, then reads the per-block
-wall-clock stamps of the last planner launch (start, phase 1 done, wait done,
-end; 100 MHz) and prints the spread of each phase over the blocks.
+wall-clock stamps of the last planner launch (8 per block, see g_plan_trace;
+100 MHz) and prints the spread of each phase over the blocks.
 
   usage: python3 tools/plan_trace_diag.py [i/N]
 """
@@ -39,20 +39,22 @@ def main():
     for _ in range(8):
         Crc32c.calculate_batch(arena, o, ln, None, out, sync=False)
     torch.cuda.synchronize()
-    buf = (ctypes.c_ulonglong * (256 * 4))()
+    buf = (ctypes.c_ulonglong * (256 * 8))()
     if _native.lib.bmqcrc_diag_plan_trace(buf) != 0:
         raise SystemExit("bmqcrc_diag_plan_trace failed")
-    t = np.array(buf, dtype=np.float64).reshape(256, 4)
+    t = np.array(buf, dtype=np.float64).reshape(256, 8)
     t = t[t[:, 0] > 0]
     t0 = t[:, 0].min()
     us = (t - t0) / 100.0  # 100 MHz ticks -> microseconds
     res = {"shard": shard, "blocks": int(t.shape[0])}
-    for k, name in enumerate(["start", "phase1_done", "wait_done", "end"]):
+    names = ["start", "loads_landed", "tile0_done", "phase1_done", "wait_done", "deferred_done",
+             "bases_done", "end"]
+    for k, name in enumerate(names):
         res[name + "_us"] = [round(float(us[:, k].min()), 2), round(float(np.median(us[:, k])), 2),
                              round(float(us[:, k].max()), 2)]
-    res["phase1_us"] = [round(float(x), 2) for x in np.percentile(us[:, 1] - us[:, 0], [0, 50, 100])]
-    res["wait_us"] = [round(float(x), 2) for x in np.percentile(us[:, 2] - us[:, 1], [0, 50, 100])]
-    res["phase2_us"] = [round(float(x), 2) for x in np.percentile(us[:, 3] - us[:, 2], [0, 50, 100])]
+    for k in range(1, len(names)):
+        res["d_" + names[k]] = [round(float(x), 2)
+                                for x in np.percentile(us[:, k] - us[:, k - 1], [0, 50, 100])]
     print(json.dumps(res))
 
 
