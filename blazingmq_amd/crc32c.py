@@ -343,7 +343,8 @@ def forget_shape(device, stream):
 def plan_wait(device, stream, wait_us=1000):
     """Longest wait (microseconds) of the single-pass planner's blocks for
     each other on (device, stream) before a ragged batch's size-class map is
-    given up (bmqcrc_plan_wait; results stay exact, the fold then searches).
+    given up (bmqcrc_plan_wait; results stay exact, the fold then takes every
+    message whole in one lane).
     Returns how many planned batches there gave up their map so far."""
     n = ctypes.c_uint64()
     _native.check(_native.lib.bmqcrc_plan_wait(device, stream.cuda_stream, int(wait_us),

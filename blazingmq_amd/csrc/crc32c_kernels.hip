@@ -861,10 +861,15 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     } else {
         __syncthreads();
     }
-    // more segments than 32-bit indices hold: every message in one lane
-    const uint32_t wholef = whole | pt.overflow;
-    if (pt.overflow) {
+    // more segments than 32-bit indices hold, or k_plan_map gave its map up
+    // (it then writes no seg_first to search): every message in one lane
+    const uint32_t wholef = whole | pt.overflow | map_void;
+    const uint32_t hint_identity = pt.identity && !pt.overflow;
+    const uint32_t hint_uni = pt.uni;
+    if (pt.overflow || map_void) {
         pt.identity = 1u;
+        pt.uni = 0u;
+        pt.total = (uint32_t)a.n;
     }
     const uint32_t total = pt.total;
     const uint32_t identity = pt.identity;
@@ -882,9 +887,10 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         // (a closed-form batch whose u segments per message divide 64 also
         // records u: its successor can run speculatively, see kHintClosed)
         __hip_atomic_store(a.shape_hint,
-                           (identity && !pt.overflow) ? kHintIdentity
-                           : (uni && !pt.overflow && 64u % uni == 0u) ? (kHintClosed | (uni << 8))
-                           : (uni || pt.overflow) ? kHintClosed
+                           hint_identity ? kHintIdentity
+                           : (hint_uni && !pt.overflow && 64u % hint_uni == 0u)
+                               ? (kHintClosed | (hint_uni << 8))
+                           : (hint_uni || pt.overflow) ? kHintClosed
                                                   : kHintRagged,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -1360,10 +1366,11 @@ __device__ __forceinline__ void unpack_quad(const Quad& q, uint64_t i0, uint64_t
 }
 
 // seg_first (exclusive prefix from r) and out[] initialisation of one
-// planner thread's quad: one dwordx4 store each for a whole quad.  out gets
-// 0 for every non-empty message (a one-segment message is stored whole by
-// its lane in k_fold, later on the stream; others XOR-accumulate from 0) and
-// the seed for an empty one.
+// planner thread's quad: one dwordx4 store each for a whole quad, out only
+// when the quad holds a message of other than one segment.  out gets 0 for
+// every non-empty message (a one-segment message is stored whole by its lane
+// in k_fold, later on the stream; others XOR-accumulate from 0) and the seed
+// for an empty one.
 __device__ __forceinline__ void store_quad(const BatchArgs& a, uint64_t i0, uint64_t hi,
                                            const uint32_t (&L)[kPlanV], const uint32_t (&ns)[kPlanV],
                                            uint32_t r, bool write_sf)
@@ -1382,7 +1389,9 @@ __device__ __forceinline__ void store_quad(const BatchArgs& a, uint64_t i0, uint
         if (write_sf) {
             *(u32x4e*)(a.seg_first + i0) = u32x4{sf[0], sf[1], sf[2], sf[3]};
         }
-        *(u32x4e*)(a.out + i0) = u32x4{o[0], o[1], o[2], o[3]};
+        if ((ns[0] != 1u) | (ns[1] != 1u) | (ns[2] != 1u) | (ns[3] != 1u)) {
+            *(u32x4e*)(a.out + i0) = u32x4{o[0], o[1], o[2], o[3]};
+        }
         return;
     }
 #pragma unroll
@@ -1391,7 +1400,9 @@ __device__ __forceinline__ void store_quad(const BatchArgs& a, uint64_t i0, uint
             if (write_sf) {
                 a.seg_first[i0 + v] = sf[v];
             }
-            a.out[i0 + v] = o[v];
+            if (ns[v] != 1u) {
+                a.out[i0 + v] = o[v];
+            }
         }
     }
 }
@@ -1736,10 +1747,11 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_sort(BatchArgs a)
 // GPU at once, but nothing guarantees it (other streams, other processes).
 // A block that has waited map_wait_ticks (1 ms by default, bmqcrc_plan_wait)
 // without seeing every arrival marks the map invalid for this launch
-// (plan_sync[2] = epoch, plan_sync[3] counts such launches), writes its
-// seg_first and leaves; k_fold then ignores seginfo and maps segments by
-// binary search over seg_first.  Arrival flags carry the launch's epoch, so
-// nothing needs resetting between launches.
+// (plan_sync[2] = epoch, plan_sync[3] counts such launches) and leaves;
+// k_fold then ignores the planner's output and folds every message whole in
+// one lane (the schedule of BMQCRC_F_WHOLE_MESSAGES: exact, slower).  With
+// the map in use seg_first is not written.  Arrival flags carry the launch's
+// epoch, so nothing needs resetting between launches.
 #ifndef BMQCRC_MAP_REG_TILES
 #define BMQCRC_MAP_REG_TILES 4
 #endif
@@ -1914,12 +1926,13 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
     // a single-tile block whose messages all have the same segment count
     // leaves seg_first to the consumers (seg_first_g), as in k_plan
     const bool write_sf = !one_tile || sh[2] != sh[3];
-    // the register tiles' deferred writes (every exit after the wait runs them)
-    auto deferred = [&]() {
+    // the register tiles' deferred writes: out[], and seg_first when there
+    // is no map to use
+    auto deferred = [&](bool sf) {
 #pragma unroll
         for (uint32_t t = 0; t < kMapRegTiles; ++t) {
             if (t < ntiles) {
-                tile_words(lo + (uint64_t)t * kTile, Lr[t], R0[t], write_sf);
+                tile_words(lo + (uint64_t)t * kTile, Lr[t], R0[t], sf && write_sf);
             }
         }
     };
@@ -1993,7 +2006,8 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
     __syncthreads();
     PLAN_STAMP(4)
     if (!go) {
-        deferred();
+        // the map is given up: k_fold folds every message whole in one lane
+        // and stores it plainly (no seg_first, no out[] initialisation)
         return;
     }
     // Batch shape and size from every block's words: closed-form batches and
@@ -2046,10 +2060,11 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
             map = all <= min((unsigned long long)a.max_segs, (unsigned long long)kSegLimit);
         }
     }
-    // seg_first is written even with the map: another block may have given
-    // the map up after this one saw every arrival (its timer ran out between
-    // two polls), and then k_fold searches seg_first for every block.
-    deferred();
+    // seg_first only without a map (k_fold then uses closed forms or
+    // searches it).  With the map it is never read: should another block
+    // give the map up after this one saw every arrival (its timer ran out
+    // between two polls), k_fold folds every message whole instead.
+    deferred(!map);
     PLAN_STAMP(5)
     if (!map) {
         return;

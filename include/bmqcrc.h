@@ -190,8 +190,8 @@ int bmqcrc_forget_shape(int device, void* stream);
  * giving up the size-class map of that batch; default 1000.  The planner's
  * blocks meet once, grid-wide; when the GPU cannot run them all at once
  * (other streams or processes hold the CUs) a block that waited this long
- * leaves, and the fold then maps segments by binary search -- results are
- * exact either way, only slower.  0 gives every map up at once (a test hook
+ * leaves, and the fold then folds every message of that batch whole in one
+ * lane -- results are exact either way, only slower.  0 gives every map up at once (a test hook
  * for that path).  *voided (may be NULL) receives how many planned batches on
  * (device, stream) gave up their map so far; asking for it waits for the
  * work already enqueued on that stream. */
