@@ -27,8 +27,7 @@ constexpr int kBuckets = 16;            // segment size classes: floor(log2(line
 // forces 2, bit4 always builds the size-class map (no shape prediction),
 // bit5 reads one- and two-line groups non-temporally too, bit7 plans ragged
 // batches with the round-2 pair k_plan<true> + k_plan_sort instead of the
-// single-pass k_plan_map, bit9 plans them with k_plan_map even when its
-// blocks hold a single tile.
+// single-pass k_plan_map.
 #ifndef BMQCRC_TUNE_BITS
 #define BMQCRC_TUNE_BITS 0u
 #endif
@@ -98,12 +97,14 @@ struct BatchArgs {
 constexpr uint32_t kPlanV = 4;  // planner: messages per thread per tile (kPlanBlock * kPlanV)
 constexpr uint32_t kSegLast = 0x80000000u;  // seginfo: the entry is its message's last segment
 
-// Ragged batches (map_planned): the single-pass k_plan_map when its blocks
-// hold more than one tile, else the round-2 pair k_plan<true> + k_plan_sort
-// (TUNE bit 7 forces the pair).
+// Ragged batches (map_planned): the single-pass k_plan_map (TUNE bit 7: the
+// round-2 pair k_plan<true> + k_plan_sort instead; the pair was kept for
+// single-tile blocks until the round-3 planner work made k_plan_map faster
+// there too: 19.7 against 24.2 us on the 1/8 Zipf shard,
+// profiles/r03/ab/planner_stamps/).
 inline bool single_pass_planner(const BatchArgs& a)
 {
-    return (a.per_msg > (uint64_t)kPlanBlock * kPlanV || (a.tune & 512u)) && !(a.tune & 128u);
+    return !(a.tune & 128u);
 }
 
 constexpr uint32_t kHintUnknown = 0;

@@ -1793,7 +1793,7 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
     __shared__ uint32_t sh[4];
     __shared__ uint32_t hist[kBuckets];
     __shared__ uint32_t run[kBuckets];
-    __shared__ uint32_t part[2][kPlanBlock / kBuckets][kBuckets];
+    __shared__ uint32_t part[2][2][kBuckets];  // per wave: class totals / prefix, block words
     __shared__ unsigned long long segs64;
     __shared__ uint32_t go;
     __shared__ PlanTail tail;
@@ -2010,54 +2010,74 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
         // and stores it plainly (no seg_first, no out[] initialisation)
         return;
     }
-    // Batch shape and size from every block's words: closed-form batches and
-    // those past seginfo's capacity (or 32-bit indices) need no map.
-    // Every load of the other blocks' words goes out at once: the block
-    // words for the shape and size, and this thread's histogram entries for
-    // the class bases below (c = thread % 16, blocks b = thread / 16 + 64 k).
-    static_assert(kPlanBlock % kBuckets == 0 && kPlanMaxBlocks <= 4 * (kPlanBlock / kBuckets),
-                  "bucket-base reduction layout");
-    constexpr uint32_t kParts = kPlanBlock / kBuckets;
+    // Batch shape and size from every block's words (closed-form batches
+    // and those past seginfo's capacity or 32-bit indices need no map), and
+    // this block's slice of every class (k_plan_sort's class-major order):
+    // every load goes out at once, each wave reduces its share by DPP, and
+    // one LDS exchange combines the waves.  Wave c sums class c over all
+    // blocks (lane l: blocks l + 64 k); the block words are in waves 0-3.
+    static_assert(kPlanBlock / 64 == kBuckets && kPlanMaxBlocks <= 4 * 64,
+                  "one wave per size class, four blocks per lane");
+    const uint32_t cw = threadIdx.x >> 6;
     uint32_t hb[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t b = (uint32_t)lane + 64u * k;
+        hb[k] = b < nb ? __hip_atomic_load(&a.bhist[(uint64_t)b * kBuckets + cw], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT)
+                       : 0u;
+    }
+    auto word = [&](uint32_t w) {
+        return __hip_atomic_load(&a.block_sum[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    const uint32_t j = threadIdx.x;
+    const uint32_t u0 = word(2u * nb);
+    const uint32_t v = j < nb ? word(j) : 0u;
+    const uint32_t nn = j < nb ? word(nb + j) : 0u;
+    const uint32_t u = j < nb ? word(2u * nb + j) : u0;
     {
-        const uint32_t c = threadIdx.x % kBuckets, pi = threadIdx.x / kBuckets;
+        uint32_t tot = 0, pre = 0;
 #pragma unroll
         for (uint32_t k = 0; k < 4; ++k) {
-            const uint32_t b = pi + kParts * k;
-            hb[k] = b < nb ? __hip_atomic_load(&a.bhist[(uint64_t)b * kBuckets + c],
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                           : 0u;
+            tot += hb[k];
+            pre += (uint32_t)lane + 64u * k < bid ? hb[k] : 0u;
+        }
+        tot = wave_sum(tot);
+        pre = wave_sum(pre);
+        // (a block over the limit stores ~0: its wave's sum passes any capacity)
+        const uint64_t segs = wave_sum64(v);
+        const bool w_ragged = __ballot(nn != 0u) != 0, w_mixed = __ballot(u != u0) != 0;
+        if (lane == 0) {
+            part[0][0][cw] = tot;
+            part[1][0][cw] = pre;
+            part[0][1][cw] = (uint32_t)min(segs, (uint64_t)0xffffffffu);
+            part[1][1][cw] = (w_ragged ? 1u : 0u) | (w_mixed ? 2u : 0u);
         }
     }
+    __syncthreads();
     bool map = true;
     {
-        const uint32_t j = threadIdx.x;
-        auto word = [&](uint32_t w) {
-            return __hip_atomic_load(&a.block_sum[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        };
-        const uint32_t v = j < nb ? word(j) : 0u;
-        const uint32_t nn = j < nb ? word(nb + j) : 0u;
-        const uint32_t u0 = word(2u * nb);
-        const uint32_t u = j < nb ? word(2u * nb + j) : u0;
-        const int ragged = __syncthreads_or(nn != 0u);
-        const int mixed = __syncthreads_or(u != u0);
+        uint32_t flags = 0;
+        unsigned long long all = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < (uint32_t)kBuckets; ++w) {
+            flags |= part[1][1][w];
+            all += part[0][1][w];
+        }
+        const bool ragged = flags & 1u, mixed = flags & 2u;
         if (!ragged || (!mixed && u0 != 0xffffffffu)) {
             map = false;  // identity or uniform: k_fold uses closed forms
         } else {
-            // (a block over the limit counts as 2^32, past any capacity)
-            const unsigned long long sum =
-                wave_sum64(v) + (v == 0xffffffffu ? 1ull : 0ull);
-            if (lane == 0) {
-                wsum[threadIdx.x >> 6] = (uint32_t)min(sum, (unsigned long long)0xffffffffu);
-            }
-            __syncthreads();
-            unsigned long long all = 0;
-            for (uint32_t w = 0; w < (uint32_t)(kPlanBlock >> 6); ++w) {
-                all += wsum[w];
-            }
             // past seginfo's capacity: k_fold searches seg_first (or folds
             // whole messages past 32-bit segment indices)
             map = all <= min((unsigned long long)a.max_segs, (unsigned long long)kSegLimit);
+        }
+        if (threadIdx.x < kBuckets) {
+            uint32_t acc = 0;
+            for (uint32_t c = 0; c < threadIdx.x; ++c) {
+                acc += part[0][0][c];
+            }
+            run[threadIdx.x] = acc + part[1][0][threadIdx.x];
         }
     }
     // seg_first only without a map (k_fold then uses closed forms or
@@ -2069,37 +2089,7 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
     if (!map) {
         return;
     }
-    // This block's slice of every class (k_plan_sort's bucket-major order).
-    {
-        const uint32_t c = threadIdx.x % kBuckets, pi = threadIdx.x / kBuckets;
-        uint32_t tot = 0, pre = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-            tot += hb[k];
-            pre += pi + kParts * k < bid ? hb[k] : 0u;
-        }
-        part[0][pi][c] = tot;
-        part[1][pi][c] = pre;
-        __syncthreads();
-        if (threadIdx.x < kBuckets) {
-            uint32_t t = 0, q = 0;
-            for (uint32_t pp = 0; pp < kParts; ++pp) {
-                t += part[0][pp][threadIdx.x];
-                q += part[1][pp][threadIdx.x];
-            }
-            part[0][0][threadIdx.x] = t;
-            part[1][0][threadIdx.x] = q;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t acc = 0;
-            for (int cc = 0; cc < kBuckets; ++cc) {
-                run[cc] = acc + part[1][0][cc];
-                acc += part[0][0][cc];
-            }
-        }
-        __syncthreads();
-    }
+    __syncthreads();  // run[]
     PLAN_STAMP(6)
     // Phase 2: (message, k) of every segment.
     auto write_tile = [&](uint32_t t, const uint32_t (&L)[kPlanV], uint32_t cls) {

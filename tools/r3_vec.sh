@@ -1,6 +1,6 @@
 #!/bin/bash
-# Planner round: GPU suite on the product, parity + fuzz with the single-pass
-# planner forced on single-tile blocks (variant_sp), phase stamps, and traced
+# Planner round: GPU suite on the product, parity + fuzz with the ragged
+# planner replaced by the round-2 pair (variant_pair), phase stamps, and traced
 # planner times on Zipf and its 1/8 shard.
 #   usage (on the box): tools/r3_vec.sh <tag>
 set -o pipefail
@@ -12,16 +12,16 @@ L=blazingmq_amd/lib
 T="python3 -u -m pytest -x -q --timeout 300 --timeout-method thread"
 timeout -k 10 400 $T tests -m gpu > gpurun_out/${tag}_gputests.log 2>&1 || { echo "gpu suite failed"; tail -20 gpurun_out/${tag}_gputests.log; exit 1; }
 tail -1 gpurun_out/${tag}_gputests.log
-if [ -f $L/variant_sp.so ]; then
+if [ -f $L/variant_pair.so ]; then
   cp $L/libbmqcrc.so /tmp/vec_base.so
-  cp $L/variant_sp.so $L/libbmqcrc.so
-  timeout -k 10 400 $T tests/test_gpu_parity.py tests/test_gpu_fuzz.py -m gpu > gpurun_out/${tag}_sp_tests.log 2>&1
+  cp $L/variant_pair.so $L/libbmqcrc.so
+  timeout -k 10 400 $T tests/test_gpu_parity.py tests/test_gpu_fuzz.py -m gpu -k "not map_given_up and not single_pass_planner" > gpurun_out/${tag}_sp_tests.log 2>&1
   rc=$?
   cp /tmp/vec_base.so $L/libbmqcrc.so
   tail -1 gpurun_out/${tag}_sp_tests.log
   [ $rc -eq 0 ] || { tail -20 gpurun_out/${tag}_sp_tests.log; exit 1; }
 fi
-timeout -k 10 300 tools/r3_stamps.sh gpurun_out/${tag}_stamps.jsonl > /dev/null || exit 1
+timeout -k 10 300 tools/r3_stamps.sh gpurun_out/${tag}_stamps.jsonl pd3 pd3 > /dev/null || exit 1
 for args in "--config zipf_4M" "--config zipf_4M --shard 7/8"; do
   t=$(echo "$args" | tr -c 'a-zA-Z0-9_\n' '_')
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_tr$t -o run --output-format csv -- \
