@@ -1290,8 +1290,20 @@ __device__ __forceinline__ uint32_t msg_segments(const BatchArgs& a, uint64_t of
     }
     const uint32_t SEG = a.seg_bytes;
     const uint32_t nseg = (seg_shift ? ((len - 1u) >> seg_shift) : (len - 1u) / SEG) + 1u;
-    const SegGeom geo = seg_geom((uint64_t)(uintptr_t)a.arena + off, len, nseg - 1u, nseg, SEG);
-    *c_last = size_class(geo.nl);
+    // seg_geom's line count of the last segment in 32-bit arithmetic: it
+    // depends only on the segment's start offset in its line (the message's
+    // for k = 0, else 0: internal boundaries are line-aligned) and its
+    // length D = E - S (for k > 0: len - k SEG + the message's offset in its
+    // line), both < 2^31 (tests/test_fold_model.py::test_last_segment_class)
+    const uint32_t k = nseg - 1u;
+    const uint32_t s0 = ((uint32_t)(uintptr_t)a.arena + (uint32_t)off) & 127u;
+    const uint32_t s = k ? 0u : s0;
+    const uint32_t D = k ? len - (seg_shift ? k << seg_shift : k * SEG) + s0 : len;
+    const uint32_t dn = (k == 0u && D < 4u) ? 4u : D;
+    const uint32_t pe = (s + dn + 15u) & ~15u;
+    const uint32_t nl_r = (pe - (s & ~15u) + 127u) >> 7;
+    const uint32_t nl_l = (s + dn + 127u) >> 7;
+    *c_last = size_class((kRightAlign && (nl_r < nl_l || nl_r <= kRightAlignLines)) ? nl_r : nl_l);
     return nseg;
 }
 

@@ -422,3 +422,41 @@ def test_four_byte_seginfo_round_trip():
         got = _decode_groups(entries, firstk)
         assert got == want
         assert len(full) + len(last) == len(entries)
+
+
+def last_class_nl(off_lo, ln, seg, ra_lines=1):
+    """msg_segments' 32-bit line count of a message's last segment (the
+    planner's size class input): from the message's offset in its line and
+    the segment's length only."""
+    nseg = (ln - 1) // seg + 1
+    k = nseg - 1
+    s0 = off_lo & 127
+    s = 0 if k else s0
+    d = (ln - k * seg + s0) if k else ln
+    dn = 4 if (k == 0 and d < 4) else d
+    pe = (s + dn + 15) & ~15
+    nl_r = (pe - (s & ~15) + 127) >> 7
+    nl_l = (s + dn + 127) >> 7
+    return nl_r if (nl_r < nl_l or nl_r <= ra_lines) else nl_l
+
+
+def test_last_segment_class():
+    """The planner's 32-bit last-segment line count equals seg_geom's (geom)
+    for the last segment, over random offsets (any 64-bit address), lengths
+    and segment sizes, including lengths near 2^32."""
+    rng = np.random.default_rng(11)
+    cases = []
+    for seg in (256, 384, 2048, 16384, 65536, 1 << 30):
+        for _ in range(400):
+            off = int(rng.integers(0, 1 << 40))
+            ln = int(rng.choice([rng.integers(1, 8), rng.integers(1, 4 * seg + 300),
+                                 rng.integers((1 << 32) - 4096, 1 << 32)]))
+            cases.append((off, ln, seg))
+    for off, ln, seg in cases:
+        nseg = (ln - 1) // seg + 1
+        k = nseg - 1
+        S = off if k == 0 else ((off + k * seg) & ~127)
+        E = off + ln
+        _, nl = geom(S, E, k == 0)
+        assert last_class_nl(off & 0xFFFFFFFF, ln, seg) == nl, (off, ln, seg)
+
