@@ -232,7 +232,7 @@ static void split_ranges(uint64_t items, uint64_t* per, uint32_t* blocks)
 }
 
 int plan_ws(Workspace* w, hipStream_t s, uint64_t n, uint64_t arena_bytes, uint32_t seg,
-            BatchArgs* a)
+            BatchArgs* a, int num_cus = 256)
 {
     const uint64_t max_segs = max_segs_for(n, arena_bytes, seg);
     split_ranges(n, &a->per_msg, &a->nblocks);
@@ -270,6 +270,12 @@ int plan_ws(Workspace* w, hipStream_t s, uint64_t n, uint64_t arena_bytes, uint3
         w->hint_dev = (uint32_t*)d;
     }
     a->shape_hint = w->hint_dev;
+    {
+        // expected k_fold groups per wave (max_segs bounds the segments)
+        const uint64_t waves = (uint64_t)(num_cus > 0 ? num_cus : 256) * a->blocks_per_cu *
+                               kWavesPerBlock;
+        a->class_desc = (max_segs / 64) < kClassDescGroupsPerWave * waves ? 1u : 0u;
+    }
     // seginfo entries hold 31-bit message indices (bit 31 marks a last
     // segment): larger batches map their segments by binary search
     a->map_planned = n < (1ull << 31) ? 1u : 0u;
@@ -396,7 +402,7 @@ int run_batch(Ctx& c, uint32_t flags, uint32_t seg, const void* arena, uint64_t 
     if (flags & BMQCRC_F_WHOLE_MESSAGES) {
         a.whole = 1;  // identity map over messages: no planner workspace
         a.max_segs = n;
-    } else if ((rc = plan_ws(w, c.s, n, arena_bytes, seg, &a))) {
+    } else if ((rc = plan_ws(w, c.s, n, arena_bytes, seg, &a, c.st->num_cus))) {
         return rc;
     } else if (!(kTuneBits & 16u) && !(flags & BMQCRC_F_PLAN)) {
         const uint32_t hint = __atomic_load_n(w->hint_host, __ATOMIC_RELAXED);

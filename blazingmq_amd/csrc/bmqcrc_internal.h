@@ -92,7 +92,16 @@ struct BatchArgs {
     unsigned long long* plan_sync;
     uint32_t plan_epoch;       // k_plan_map launch tag on this workspace, never 0
     uint64_t map_wait_ticks;   // k_plan_map's grid-wide wait limit (100 MHz wall clock)
+    uint32_t class_desc;       // k_plan_map: size classes in descending order (short schedules)
 };
+
+// k_fold groups per wave below which k_plan_map orders the size classes
+// largest first: the schedule's tail is then one-line groups instead of a
+// row of the largest ones.  Measured on Zipf shards (profiles/r03/ab/
+// class_order_*.jsonl, k_fold us, ascending -> descending): 1/16 shard 278 ->
+// 272, 1/8 531 -> 525, 1/4 1,036 -> 1,040, 1/2 2,051 -> 2,073, whole 4,082
+// -> 4,162; the crossover lies between ~15 and ~30 groups per wave.
+constexpr uint64_t kClassDescGroupsPerWave = 24;
 
 constexpr uint32_t kPlanV = 4;  // planner: messages per thread per tile (kPlanBlock * kPlanV)
 constexpr uint32_t kSegLast = 0x80000000u;  // seginfo: the entry is its message's last segment

@@ -1768,6 +1768,10 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_sort(BatchArgs a)
 #define BMQCRC_MAP_REG_TILES 4
 #endif
 constexpr uint32_t kMapRegTiles = BMQCRC_MAP_REG_TILES;  // tiles kept in registers across the wait
+#ifndef BMQCRC_CLASS_DESC
+#define BMQCRC_CLASS_DESC 0  // size-class order in seginfo: 0 by BatchArgs::class_desc (product),
+                             // 1 always descending, 2 always ascending (A/B builds)
+#endif
 #ifndef BMQCRC_PLAN_SKIP
 #define BMQCRC_PLAN_SKIP 0  // timing diagnostics with the map voided (wrong maps, exact CRCs):
                             // 1 no histogram atomics, 2 no last-segment claims, 4 no full-run
@@ -2086,8 +2090,9 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
         }
         if (threadIdx.x < kBuckets) {
             uint32_t acc = 0;
-            for (uint32_t c = 0; c < threadIdx.x; ++c) {
-                acc += part[0][0][c];
+            const bool desc = BMQCRC_CLASS_DESC == 1 || (BMQCRC_CLASS_DESC == 0 && a.class_desc);
+            for (uint32_t c = 0; c < (uint32_t)kBuckets; ++c) {
+                acc += (desc ? c > threadIdx.x : c < threadIdx.x) ? part[0][0][c] : 0u;
             }
             run[threadIdx.x] = acc + part[1][0][threadIdx.x];
         }
