@@ -226,7 +226,10 @@ static void split_ranges(uint64_t items, uint64_t* per, uint32_t* blocks)
 {
     const uint64_t tiles = std::max<uint64_t>((items + kPlanBlock - 1) / kPlanBlock, 1);
     const uint64_t nb = std::min<uint64_t>(tiles, kPlanMaxBlocks);
-    const uint64_t tiles_per = (tiles + nb - 1) / nb;
+    uint64_t tiles_per = (tiles + nb - 1) / nb;
+    if (kTuneBits & 512u) {  // A/B: whole planner tiles (kPlanV x kPlanBlock) per block
+        tiles_per = (tiles_per + kPlanV - 1) / kPlanV * kPlanV;
+    }
     *per = tiles_per * kPlanBlock;
     *blocks = (uint32_t)((tiles + tiles_per - 1) / tiles_per);
 }
