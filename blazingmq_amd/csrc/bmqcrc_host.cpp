@@ -245,7 +245,8 @@ int plan_ws(Workspace* w, hipStream_t s, uint64_t n, uint64_t arena_bytes, uint3
         (rc = w->seginfo.ensure(4 * max_segs)) ||
         (rc = w->firstk.ensure(4 * (max_segs / 64 + 2))) ||
         (rc = w->bhist.ensure(4ull * kBuckets * kPlanMaxBlocks)) ||
-        (rc = w->plan_sync.ensure(8ull * (kSyncFlags + kPlanMaxBlocks)))) {
+        (rc = w->plan_sync.ensure(8ull * (kSyncFlags + kPlanMaxBlocks +
+                                          kPlanMaxBlocks * (kBuckets + 3))))) {
         return rc;
     }
     if (w->plan_sync.fresh) {  // zero counters, no given-up epoch (stream-ordered)

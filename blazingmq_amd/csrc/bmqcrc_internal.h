@@ -86,9 +86,11 @@ struct BatchArgs {
     // guess was wrong.
     uint32_t spec;
     // Single-pass planner (k_plan_map): [2] the epoch of a launch whose map
-    // was given up (k_fold then ignores seginfo), [3] how many launches gave
-    // theirs up, [kSyncFlags + b] block b's arrival flag (the epoch of the
-    // launch it last arrived in).  Zeroed once when allocated.
+    // was given up (k_fold then folds every message whole), [3] how many
+    // launches gave theirs up, [kSyncFlags + b] block b's arrival flag (the
+    // epoch of the launch it last arrived in), then kPlanMaxBlocks x
+    // (kBuckets + 3) epoch-tagged words the blocks exchange.  Zeroed once
+    // when allocated.
     unsigned long long* plan_sync;
     uint32_t plan_epoch;       // k_plan_map launch tag on this workspace, never 0
     uint64_t map_wait_ticks;   // k_plan_map's grid-wide wait limit (100 MHz wall clock)

@@ -1816,6 +1816,20 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
     __shared__ uint32_t sruns[kPlanBlock / 64][64 * kPlanV];  // per wave: short-run ends
     const uint32_t nb = a.nblocks, ep = a.plan_epoch, bid = blockIdx.x;
     load_tail(a, min((uint64_t)bid * a.per_msg + a.per_msg, a.n), true, &tail);
+    // epoch-tagged words the blocks exchange (plan_sync after the flags),
+    // laid out for coalesced reads: [c * kPlanMaxBlocks + b] histograms,
+    // [kTagWords + i * kPlanMaxBlocks + b] block words
+    unsigned long long* const tags = a.plan_sync + kSyncFlags + kPlanMaxBlocks;
+    constexpr uint32_t kTagWords = kPlanMaxBlocks * kBuckets;
+    // mark this launch's map given up (one thread): k_fold folds every
+    // message whole; the first block to give up counts the launch
+    auto give_up = [&]() {
+        if (__hip_atomic_exchange(&a.plan_sync[2], (unsigned long long)ep, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT) != ep) {
+            __hip_atomic_fetch_add(&a.plan_sync[3], 1ull, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+    };
     unsigned long long* const sync = a.plan_sync;
     if (threadIdx.x == 0) {
         sh[1] = 0;            // messages with != 1 segment
@@ -1955,27 +1969,31 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
     // Publish the block words and the histogram, then arrive and wait.
     PLAN_STAMP(3)
     if (threadIdx.x < 64) {
-        // Wave 0 publishes the block words and the histogram with
-        // device-scope stores (they write through to memory, visible on
-        // every XCD once complete), waits for them, then arrives: one flag
-        // word per block, set to this launch's epoch.  The readers load all
-        // of it with device-scope loads, so neither side needs an agent-scope
-        // fence (an L2 write-back / invalidate: ~3 us of the wait,
-        // profiles/r03/ab/planner_stamps/).  No shared counter -- 256
-        // atomics on one word serialize at the memory side (11-16 us
-        // measured, profiles/r03/ab/planner_phases_counter_wait/) -- and no
-        // reset: a flag of an older launch holds an older epoch.
+        // Wave 0 publishes the block words and the histogram as
+        // device-scope 64-bit stores, each word tagged with this launch's
+        // epoch (they write through to memory, visible on every XCD once
+        // complete), waits for them, then arrives: one flag word per block,
+        // set to the epoch.  The readers load everything with device-scope
+        // loads and check every word's tag, reading a stale one again, so no
+        // visibility order is assumed between the flag and the words and
+        // neither side needs an agent-scope fence (an L2 write-back /
+        // invalidate: ~3 us of the wait, profiles/r03/ab/planner_stamps/).
+        // No shared counter -- 256 atomics on one word serialize at the
+        // memory side (11-16 us measured,
+        // profiles/r03/ab/planner_phases_counter_wait/) -- and no reset: a
+        // word of an older launch holds an older epoch.
+        const unsigned long long tagv = (unsigned long long)ep << 32;
         if (lane < kBuckets) {
-            __hip_atomic_store(&a.bhist[(uint64_t)bid * kBuckets + lane], hist[lane],
+            __hip_atomic_store(&tags[lane * kPlanMaxBlocks + bid], tagv | hist[lane],
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (lane == 0) {
-            __hip_atomic_store(&a.block_sum[bid], segs64 > kSegLimit ? 0xffffffffu : carry,
+        if (lane < 3) {
+            const uint32_t wv = lane == 0   ? (segs64 > kSegLimit ? 0xffffffffu : carry)
+                                : lane == 1 ? sh[1]
+                                            : (sh[2] == sh[3] ? sh[2] : 0xffffffffu);
+            __hip_atomic_store(&tags[kTagWords + lane * kPlanMaxBlocks + bid], tagv | wv,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&a.block_sum[nb + bid], sh[1], __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&a.block_sum[2u * nb + bid], sh[2] == sh[3] ? sh[2] : 0xffffffffu,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            a.block_sum[lane * nb + bid] = wv;  // for k_fold (the next launch)
         }
         __builtin_amdgcn_s_waitcnt(0);  // the stores above are complete (vmcnt 0)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -2003,12 +2021,8 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
             }
             if (wall_clock64() - t0 >= a.map_wait_ticks) {
                 ok = 0u;  // not all blocks running: give up the map, keep correctness
-                if (lane == 0 &&
-                    __hip_atomic_exchange(&sync[2], (unsigned long long)ep, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT) != ep) {
-                    // the first block of this launch to give up counts it
-                    __hip_atomic_fetch_add(&sync[3], 1ull, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
+                if (lane == 0) {
+                    give_up();
                 }
                 break;
             }
@@ -2035,42 +2049,73 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
     static_assert(kPlanBlock / 64 == kBuckets && kPlanMaxBlocks <= 4 * 64,
                   "one wave per size class, four blocks per lane");
     const uint32_t cw = threadIdx.x >> 6;
-    uint32_t hb[4];
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
-        const uint32_t b = (uint32_t)lane + 64u * k;
-        hb[k] = b < nb ? __hip_atomic_load(&a.bhist[(uint64_t)b * kBuckets + cw], __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT)
-                       : 0u;
-    }
-    auto word = [&](uint32_t w) {
-        return __hip_atomic_load(&a.block_sum[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    };
     const uint32_t j = threadIdx.x;
-    const uint32_t u0 = word(2u * nb);
-    const uint32_t v = j < nb ? word(j) : 0u;
-    const uint32_t nn = j < nb ? word(nb + j) : 0u;
-    const uint32_t u = j < nb ? word(2u * nb + j) : u0;
+    uint32_t u0 = 0;
     {
-        uint32_t tot = 0, pre = 0;
+        const uint64_t t1 = wall_clock64();
+        auto tagged = [&](const unsigned long long* p, uint32_t& val, bool& stale) {
+            const unsigned long long x = __hip_atomic_load(p, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT);
+            stale = stale || (uint32_t)(x >> 32) != ep;
+            val = (uint32_t)x;
+        };
+        while (true) {
+            bool stale = false;
+            uint32_t hb[4], v = 0, nn = 0, u;
 #pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-            tot += hb[k];
-            pre += (uint32_t)lane + 64u * k < bid ? hb[k] : 0u;
-        }
-        tot = wave_sum(tot);
-        pre = wave_sum(pre);
-        // (a block over the limit stores ~0: its wave's sum passes any capacity)
-        const uint64_t segs = wave_sum64(v);
-        const bool w_ragged = __ballot(nn != 0u) != 0, w_mixed = __ballot(u != u0) != 0;
-        if (lane == 0) {
-            part[0][0][cw] = tot;
-            part[1][0][cw] = pre;
-            part[0][1][cw] = (uint32_t)min(segs, (uint64_t)0xffffffffu);
-            part[1][1][cw] = (w_ragged ? 1u : 0u) | (w_mixed ? 2u : 0u);
+            for (uint32_t k = 0; k < 4; ++k) {
+                const uint32_t b = (uint32_t)lane + 64u * k;
+                hb[k] = 0u;
+                if (b < nb) {
+                    tagged(&tags[cw * kPlanMaxBlocks + b], hb[k], stale);
+                }
+            }
+            tagged(&tags[kTagWords + 2u * kPlanMaxBlocks], u0, stale);
+            u = u0;
+            if (j < nb) {
+                tagged(&tags[kTagWords + j], v, stale);
+                tagged(&tags[kTagWords + kPlanMaxBlocks + j], nn, stale);
+                tagged(&tags[kTagWords + 2u * kPlanMaxBlocks + j], u, stale);
+            }
+            uint32_t tot = 0, pre = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) {
+                tot += hb[k];
+                pre += (uint32_t)lane + 64u * k < bid ? hb[k] : 0u;
+            }
+            tot = wave_sum(tot);
+            pre = wave_sum(pre);
+            // (a block over the limit stores ~0: its wave's sum passes any capacity)
+            const uint64_t segs = wave_sum64(v);
+            const bool w_ragged = __ballot(nn != 0u) != 0, w_mixed = __ballot(u != u0) != 0;
+            const bool w_stale = __ballot(stale) != 0;
+            if (lane == 0) {
+                part[0][0][cw] = tot;
+                part[1][0][cw] = pre;
+                part[0][1][cw] = (uint32_t)min(segs, (uint64_t)0xffffffffu);
+                part[1][1][cw] = (w_ragged ? 1u : 0u) | (w_mixed ? 2u : 0u) | (w_stale ? 4u : 0u) |
+                                 ((threadIdx.x == 0 && wall_clock64() - t1 >= a.map_wait_ticks)
+                                      ? 8u : 0u);
+            }
+            __syncthreads();
+            uint32_t f = 0;
+#pragma unroll
+            for (uint32_t w = 0; w < (uint32_t)kBuckets; ++w) {
+                f |= part[1][1][w];
+            }
+            if (!(f & 4u)) {
+                break;
+            }
+            // a word not yet visible: read again, within the same time limit
+            if (f & 8u) {
+                if (threadIdx.x == 0) {
+                    give_up();
+                }
+                return;
+            }
+            __syncthreads();  // part[] read by all before the next round
         }
     }
-    __syncthreads();
     bool map = true;
     {
         uint32_t flags = 0;
