@@ -1778,7 +1778,8 @@ constexpr uint32_t kMapRegTiles = BMQCRC_MAP_REG_TILES;  // tiles kept in regist
                             // writes, 8 no last-segment stores
 #endif
 #ifndef BMQCRC_PLAN_DIAG
-#define BMQCRC_PLAN_DIAG 0  // 3: per-block phase stamps, 4: the same without seginfo stores
+#define BMQCRC_PLAN_DIAG 0  // 3: per-block phase stamps, 4: the same without seginfo stores,
+                            // 6: every block's first read of the exchanged words is stale
                             // (timing diagnostics, tools/plan_trace_diag.py); product: 0
 #endif
 
@@ -2059,8 +2060,15 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
             stale = stale || (uint32_t)(x >> 32) != ep;
             val = (uint32_t)x;
         };
+#if BMQCRC_PLAN_DIAG == 6
+        bool forced = true;  // diagnostic: the first read counts as stale (re-read path)
+#endif
         while (true) {
             bool stale = false;
+#if BMQCRC_PLAN_DIAG == 6
+            stale = forced;
+            forced = false;
+#endif
             uint32_t hb[4], v = 0, nn = 0, u;
 #pragma unroll
             for (uint32_t k = 0; k < 4; ++k) {
