@@ -524,10 +524,10 @@ def main():
         return e2e(args, dev, stream, arena, offs_np, lens_np, total_bytes, world, rank, dist,
                    desc)
 
-    def step(timed, plan=False):
+    def step(timed, plan=False, max_len=0):
         Crc32c.calculate_batch(arena, offsets, lengths, None, out, seg_bytes=args.seg_bytes,
                                stream=stream, sync=False, time_kernel=timed,
-                               whole_messages=args.whole_messages, plan=plan)
+                               whole_messages=args.whole_messages, plan=plan, max_len=max_len)
 
     # setup: settle the GPU clocks under this exact load (not part of W or K)
     t_settle = time.perf_counter()
@@ -562,6 +562,20 @@ def main():
     torch.cuda.synchronize(dev)
     planned = time.perf_counter() - t0
     planned_launch = bmq.last_launch(local, stream)
+    # ... and with the prediction dropped before every step but the batch's
+    # length bound declared (bmqcrc_opts.max_len, ABI 2.4): what a caller
+    # that knows its largest message pays when shapes alternate.
+    max_len = int(lens_np.max()) if n else 0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        bmq.forget_shape(local, stream)
+        step(False, max_len=max_len)
+    torch.cuda.synchronize(dev)
+    declared = time.perf_counter() - t0
+    declared_launch = bmq.last_launch(local, stream)
     if world > 1:
         dist.barrier()
     step(False)  # back to the predicted shape
@@ -578,9 +592,10 @@ def main():
     bytes_all = total_bytes
     kern_max = kern_ms / max(kern_cnt, 1)
     if world > 1:
-        tt = torch.tensor([elapsed, kern_max, planned], dtype=torch.float64)
+        tt = torch.tensor([elapsed, kern_max, planned, declared], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed, kern_max, planned = float(tt[0]), float(tt[1]), float(tt[2])
+        elapsed, kern_max, planned, declared = (float(tt[0]), float(tt[1]), float(tt[2]),
+                                                float(tt[3]))
         bt = torch.tensor([total_bytes, n], dtype=torch.int64)
         dist.all_reduce(bt)
         bytes_all, n_all = int(bt[0]), int(bt[1])
@@ -647,6 +662,13 @@ def main():
             "planned_value": round(bytes_all / 2**30 * args.steps / planned, 2),
             "planned_kernels_per_step": planned_launch["kernels"],
         }
+        # the bound buys one launch only when it fits one segment; otherwise
+        # an in-flight batch may restore the dropped prediction mid-loop, so
+        # the leg is not reported
+        if max_len <= declared_launch["seg_bytes"]:
+            res.update({"declared_max_len": max_len,
+                        "declared_ms_per_step": round(1e3 * declared / args.steps, 4),
+                        "declared_kernels_per_step": declared_launch["kernels"]})
         if rehearsal:
             res["rehearsal_single_gpu"] = True
             res["ranks_on_one_gpu"] = world

@@ -389,7 +389,9 @@ uint64_t max_length(const uint32_t* lengths, uint64_t n)
     return m;
 }
 
-// host_max_len: the longest message when the lengths were seen on the host
+// host_max_len: the longest message when the lengths were seen on the host, or
+// the caller's declared bound for device lengths (bmqcrc_opts.max_len: a
+// message over it is still exact, folded by its wave's second pass)
 // (host-buffer calls), UINT64_MAX when they live on the device.
 int run_batch(Ctx& c, uint32_t flags, uint32_t seg, const void* arena, uint64_t arena_bytes,
               const uint64_t* offsets, const uint32_t* lengths, const uint32_t* seeds,
@@ -475,9 +477,11 @@ int stage(Ctx& c, DevBuf& buf, const void* host, uint64_t bytes)
     return 0;
 }
 
+// declared_max: the caller's bound on every length of a device-resident batch
+// (bmqcrc_opts.max_len, 0 = none); host batches use the lengths they hold.
 int batch_one(int dev, void* user_stream, uint32_t flags, uint32_t seg, const void* arena,
               uint64_t arena_bytes, const uint64_t* offsets, const uint32_t* lengths,
-              const uint32_t* seeds, uint32_t* out, uint64_t n)
+              const uint32_t* seeds, uint32_t* out, uint64_t n, uint32_t declared_max = 0)
 {
     Ctx c;
     int rc = open_ctx(dev, user_stream, &c);
@@ -488,7 +492,8 @@ int batch_one(int dev, void* user_stream, uint32_t flags, uint32_t seg, const vo
     std::lock_guard<std::mutex> g(w->mu);
     const bool dev_ptrs = (flags & BMQCRC_F_DEVICE_PTRS) != 0;
     if (dev_ptrs) {
-        if ((rc = run_batch(c, flags, seg, arena, arena_bytes, offsets, lengths, seeds, out, n))) {
+        if ((rc = run_batch(c, flags, seg, arena, arena_bytes, offsets, lengths, seeds, out, n,
+                            declared_max ? (uint64_t)declared_max : UINT64_MAX))) {
             return rc;
         }
         if (!(flags & BMQCRC_F_ASYNC)) {
@@ -641,7 +646,7 @@ int bmqcrc_crc32c_batch(const void* arena, uint64_t arena_bytes, const uint64_t*
                                          o.devices, (int)o.ndevices, seg);
     }
     return batch_one(dev, o.stream, o.flags, seg, arena, arena_bytes, offsets, lengths, seeds,
-                     out, n);
+                     out, n, (o.flags & BMQCRC_F_DEVICE_PTRS) ? o.max_len : 0u);
 }
 
 int bmqcrc_crc32c_verify(const void* arena, uint64_t arena_bytes, const uint64_t* offsets,
@@ -1668,7 +1673,7 @@ uint64_t bmqcrc_host_fallbacks(int32_t* last_rc)
 
 uint32_t bmqcrc_version(void)
 {
-    return (2u << 16) | 3u;
+    return (2u << 16) | 4u;
 }
 
 }  // extern "C"

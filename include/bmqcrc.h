@@ -83,6 +83,16 @@ typedef struct bmqcrc_opts {
      * 2.0 (smaller struct_size) get 0. */
     uint32_t ndevices;
     const int32_t* devices;
+    /* ABI 2.4.  bmqcrc_crc32c_batch with BMQCRC_F_DEVICE_PTRS: the caller's
+     * upper bound on every lengths[i] (0 = none declared).  When it fits one
+     * segment the batch is ONE fold launch with no planner, whatever the
+     * previous batch on (device, stream) looked like -- the device-resident
+     * counterpart of what a host-buffer batch gets from its seen lengths (a
+     * broker knows its maximum PUT payload; its lengths live in HBM).  A
+     * message longer than the bound is still computed exactly (its wave folds
+     * it in a second pass), only slower.  BMQCRC_F_PLAN takes precedence.
+     * Callers built against ABI <= 2.3 (smaller struct_size) get 0. */
+    uint32_t max_len;
 } bmqcrc_opts;
 
 /* ---- scalar (host CPU) -------------------------------------------------- */
@@ -224,7 +234,7 @@ const char* bmqcrc_last_error(void);
 void bmqcrc_note_host_fallback(int32_t rc);
 uint64_t bmqcrc_host_fallbacks(int32_t* last_rc);
 
-/* ABI version: (major << 16) | minor (2.3). */
+/* ABI version: (major << 16) | minor (2.4). */
 uint32_t bmqcrc_version(void);
 
 #ifdef __cplusplus

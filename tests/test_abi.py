@@ -56,3 +56,21 @@ def test_version_and_error_string():
     assert lib.bmqcrc_version() >> 16 == 2
     lib.bmqcrc_last_error.restype = ctypes.c_char_p
     assert isinstance(lib.bmqcrc_last_error(), bytes)
+
+
+def test_opts_layout_matches_the_header(tmp_path):
+    # bmqcrc_opts as the C compiler lays it out (ABI 2.4 appends max_len) and
+    # as the ctypes binding does: same size, same field offsets
+    from blazingmq_amd import _native as N
+    src = tmp_path / "opts.c"
+    src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "bmqcrc.h"\n'
+                   'int main(void) { printf("%zu %zu %zu %zu\\n", sizeof(bmqcrc_opts), '
+                   'offsetof(bmqcrc_opts, ndevices), offsetof(bmqcrc_opts, devices), '
+                   'offsetof(bmqcrc_opts, max_len)); return 0; }\n')
+    exe = tmp_path / "opts"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)],
+                   check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True,
+                                          check=True).stdout.split()]
+    assert got == [ctypes.sizeof(N.Opts), N.Opts.ndevices.offset, N.Opts.devices.offset,
+                   N.Opts.max_len.offset]

@@ -598,6 +598,50 @@ def test_speculative_single_launch(cuda):
         run(lens, tag)
 
 
+def test_declared_max_len_single_launch(cuda):
+    """bmqcrc_opts.max_len (ABI 2.4): a device-resident batch whose declared
+    bound fits one segment is ONE k_fold launch even right after a ragged
+    batch on the same stream (no shape history needed); a bound that some
+    messages break, or no bound, stays bit-exact against the oracle."""
+    import torch
+    from blazingmq_amd.crc32c import last_launch
+    rng = np.random.default_rng(91)
+    arena_np = rng.integers(0, 256, size=64 << 20, dtype=np.uint8)
+    arena = torch.from_numpy(arena_np).to(cuda)
+    s = torch.cuda.Stream(cuda)
+    n = 300_000
+
+    def run(lens, tag, **kw):
+        lens = np.asarray(lens, np.uint32)
+        offs = np.array(rng.integers(0, arena_np.size - lens.astype(np.int64) + 1), np.int64)
+        seeds = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64).astype(np.uint32)
+        got = Crc32c.calculate_batch(arena, torch.from_numpy(offs).to(cuda),
+                                     torch.from_numpy(lens.view(np.int32)).to(cuda),
+                                     torch.from_numpy(seeds.view(np.int32)).to(cuda),
+                                     stream=s, **kw)
+        s.synchronize()
+        exp = oracle.batch(arena_np, offs, lens, seeds, nthreads=8)
+        bad = np.nonzero(got.cpu().numpy().view(np.uint32) != exp)[0]
+        assert bad.size == 0, (tag, [(int(i), int(lens[i])) for i in bad[:8]])
+        return last_launch(cuda.index, s)
+
+    ragged = lambda: np.minimum(rng.zipf(1.5, size=n) * 64, 1 << 20)  # noqa: E731
+    short = lambda: rng.integers(0, 257, size=n)  # noqa: E731
+    assert run(ragged(), "ragged")["kernels"] >= 2
+    ll = run(short(), "declared after ragged", max_len=256)
+    assert ll["kernels"] == 1 and ll["spec"] == 1, ll
+    assert run(ragged(), "ragged again")["kernels"] >= 2
+    broken = short()
+    broken[rng.integers(0, n, size=50)] = rng.integers(300, 200_000, size=50)
+    ll = run(broken, "declared bound broken", max_len=256)
+    assert ll["kernels"] == 1, ll
+    assert run(short(), "after a broken bound, planned")["kernels"] >= 2
+    # a bound beyond one segment is only a bound: the launch is planned
+    assert run(ragged(), "bound over a segment", max_len=1 << 20)["kernels"] >= 2
+    # BMQCRC_F_PLAN takes precedence
+    assert run(short(), "plan wins", max_len=256, plan=True)["kernels"] >= 2
+
+
 def test_ranks_shard_a_batch_on_the_gpu(cuda):
     """N ranks, one process each (torch.distributed.run, gloo for the result
     hand-off only), each CRCs its byte-balanced slice of one Zipf batch
