@@ -1,8 +1,9 @@
 """Randomized parity (the reference's fuzz harness, s_bmqfuzz_bmqp_crc32c.fuzz.cpp,
 generalised to batches): random arenas, message counts, lengths from several
 distributions (empty, < 4 bytes, line-edge sizes, multi-segment), random
-offsets (unaligned, overlapping), random seeds and segment sizes, and the
-whole-messages flag -- every CRC compared with the oracle.  BMQCRC_FUZZ_ROUNDS
+offsets (unaligned, overlapping), random seeds and segment sizes, the
+whole-messages flag and declared length bounds (exact, broken, loose) -- every
+CRC compared with the oracle.  BMQCRC_FUZZ_ROUNDS
 scales the number of batches (default 24), BMQCRC_FUZZ_MAX_N and
 BMQCRC_FUZZ_ARENA their size."""
 import os
@@ -48,15 +49,20 @@ def test_fuzz_batch(cuda, round_):
         if rng.integers(0, 2) else None
     seg = int(rng.choice([0, 0, 256, 384, 1024, 4096, 16384, 65536]))
     whole = bool(rng.integers(0, 4) == 0)
+    # declared length bound (bmqcrc_opts.max_len): none, exact, broken, loose
+    mk = int(rng.integers(0, 4))
+    top = int(lens.max(initial=0))
+    max_len = [0, top, int(np.median(lens)) if n else 0, top + 4096][mk]
     exp = oracle.batch(arena, offs, lens, seeds, nthreads=8)
     a = torch.from_numpy(arena).to(cuda)
     o = torch.from_numpy(offs.astype(np.int64)).to(cuda)
     ln = torch.from_numpy(lens.view(np.int32)).to(cuda)
     sd = None if seeds is None else torch.from_numpy(seeds.view(np.int32)).to(cuda)
-    got = Crc32c.calculate_batch(a, o, ln, sd, seg_bytes=seg, whole_messages=whole)
+    got = Crc32c.calculate_batch(a, o, ln, sd, seg_bytes=seg, whole_messages=whole,
+                                 max_len=max_len)
     got = got.cpu().numpy().view(np.uint32)
     bad = np.nonzero(got != exp)[0]
-    assert bad.size == 0, (round_, n, seg, whole, bad[:5], lens[bad[:5]], offs[bad[:5]])
+    assert bad.size == 0, (round_, n, seg, whole, max_len, bad[:5], lens[bad[:5]], offs[bad[:5]])
 
 
 @pytest.mark.parametrize("round_", range(max(2, ROUNDS // 8)))
