@@ -524,10 +524,11 @@ def main():
         return e2e(args, dev, stream, arena, offs_np, lens_np, total_bytes, world, rank, dist,
                    desc)
 
-    def step(timed, plan=False, max_len=0):
+    def step(timed, plan=False, max_len=0, min_len=0):
         Crc32c.calculate_batch(arena, offsets, lengths, None, out, seg_bytes=args.seg_bytes,
                                stream=stream, sync=False, time_kernel=timed,
-                               whole_messages=args.whole_messages, plan=plan, max_len=max_len)
+                               whole_messages=args.whole_messages, plan=plan, max_len=max_len,
+                               min_len=min_len)
 
     # setup: settle the GPU clocks under this exact load (not part of W or K)
     t_settle = time.perf_counter()
@@ -563,16 +564,17 @@ def main():
     planned = time.perf_counter() - t0
     planned_launch = bmq.last_launch(local, stream)
     # ... and with the prediction dropped before every step but the batch's
-    # length bound declared (bmqcrc_opts.max_len, ABI 2.4): what a caller
-    # that knows its largest message pays when shapes alternate.
+    # length bounds declared (bmqcrc_opts.max_len / min_len, ABI 2.4): what a
+    # caller that knows its message sizes pays when shapes alternate.
     max_len = int(lens_np.max()) if n else 0
+    min_len = int(lens_np.min()) if n else 0
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         bmq.forget_shape(local, stream)
-        step(False, max_len=max_len)
+        step(False, max_len=max_len, min_len=min_len)
     torch.cuda.synchronize(dev)
     declared = time.perf_counter() - t0
     declared_launch = bmq.last_launch(local, stream)
@@ -662,11 +664,13 @@ def main():
             "planned_value": round(bytes_all / 2**30 * args.steps / planned, 2),
             "planned_kernels_per_step": planned_launch["kernels"],
         }
-        # the bound buys one launch only when it fits one segment; otherwise
-        # an in-flight batch may restore the dropped prediction mid-loop, so
-        # the leg is not reported
-        if max_len <= declared_launch["seg_bytes"]:
-            res.update({"declared_max_len": max_len,
+        # the bounds buy one launch only when every length in them has the
+        # same u segments, u dividing 64; otherwise an in-flight batch may
+        # restore the dropped prediction mid-loop, so the leg is not reported
+        sb = max(declared_launch["seg_bytes"], 1)
+        u_hi, u_lo = (max_len - 1) // sb + 1, (max(min_len, 1) - 1) // sb + 1
+        if max_len and (u_hi == 1 or (min_len and u_hi == u_lo and 64 % u_hi == 0)):
+            res.update({"declared_max_len": max_len, "declared_min_len": min_len,
                         "declared_ms_per_step": round(1e3 * declared / args.steps, 4),
                         "declared_kernels_per_step": declared_launch["kernels"]})
         if rehearsal:

@@ -32,7 +32,8 @@ class Opts(ctypes.Structure):
     _fields_ = [("struct_size", ctypes.c_uint32), ("device", ctypes.c_int32),
                 ("stream", ctypes.c_void_p), ("flags", ctypes.c_uint32),
                 ("seg_bytes", ctypes.c_uint32), ("ndevices", ctypes.c_uint32),
-                ("devices", ctypes.c_void_p), ("max_len", ctypes.c_uint32)]
+                ("devices", ctypes.c_void_p), ("max_len", ctypes.c_uint32),
+                ("min_len", ctypes.c_uint32)]
 
 
 # One HIP runtime per process: when PyTorch-ROCm is present it ships its own
@@ -132,10 +133,11 @@ def check_count(n):
     return n
 
 
-def make_opts(device=-1, stream=None, flags=0, seg_bytes=0, devices=None, max_len=0):
+def make_opts(device=-1, stream=None, flags=0, seg_bytes=0, devices=None, max_len=0,
+              min_len=0):
     """bmqcrc_opts; `devices` (a sequence of ordinals, repeats allowed) spreads
     the format-walk entry points over several devices (ABI 2.1); `max_len`
-    declares a bound on a device-resident batch's lengths (ABI 2.4)."""
+    and `min_len` declare bounds on a device-resident batch's lengths (ABI 2.4)."""
     o = Opts()
     o.struct_size = ctypes.sizeof(Opts)
     o.device = device
@@ -143,6 +145,7 @@ def make_opts(device=-1, stream=None, flags=0, seg_bytes=0, devices=None, max_le
     o.flags = flags
     o.seg_bytes = seg_bytes
     o.max_len = max_len
+    o.min_len = min_len
     if devices is not None and len(devices) > 1:
         arr = (ctypes.c_int32 * len(devices))(*devices)
         o._devices_keep = arr  # the array lives as long as the opts

@@ -114,7 +114,7 @@ class Crc32c:
     @staticmethod
     def calculate_batch(arena, offsets, lengths, seeds=None, out=None, *, seg_bytes=0,
                         device=None, stream=None, sync=True, time_kernel=False,
-                        whole_messages=False, devices=None, plan=False, max_len=0):
+                        whole_messages=False, devices=None, plan=False, max_len=0, min_len=0):
         """Batched CRC32-C of messages ``arena[offsets[i] : offsets[i]+lengths[i]]``.
 
         torch CUDA tensors: ``arena`` uint8, ``offsets`` int64, ``lengths`` /
@@ -128,7 +128,9 @@ class Crc32c:
         batch instead of predicting its shape from the previous batch.
         ``max_len`` (bmqcrc_opts.max_len, device tensors): the caller's bound
         on every length; when it fits one segment the batch is one launch
-        whatever the previous batch was (a longer message stays exact).
+        whatever the previous batch was (a longer message stays exact);
+        with ``min_len`` too, a range whose lengths all have the same u
+        segments (u dividing 64) gets the uniform single launch.
         """
         try:
             import torch
@@ -136,13 +138,13 @@ class Crc32c:
             torch = None
         if torch is not None and isinstance(arena, torch.Tensor) and arena.is_cuda:
             return _batch_torch(torch, arena, offsets, lengths, seeds, out, seg_bytes, stream,
-                                sync, time_kernel, whole_messages, plan, max_len)
+                                sync, time_kernel, whole_messages, plan, max_len, min_len)
         return _batch_host(arena, offsets, lengths, seeds, out, seg_bytes, device,
                            whole_messages, devices)
 
 
 def _batch_torch(torch, arena, offsets, lengths, seeds, out, seg_bytes, stream, sync,
-                 time_kernel=False, whole_messages=False, plan=False, max_len=0):
+                 time_kernel=False, whole_messages=False, plan=False, max_len=0, min_len=0):
     dev = arena.device
     n = offsets.numel()
     for name, t, dt in (("offsets", offsets, torch.int64), ("lengths", lengths, torch.int32)):
@@ -170,7 +172,7 @@ def _batch_torch(torch, arena, offsets, lengths, seeds, out, seg_bytes, stream, 
         flags |= _native.BMQCRC_F_PLAN
     o = _native.make_opts(device=dev.index if dev.index is not None else -1,
                           stream=stream.cuda_stream, flags=flags, seg_bytes=seg_bytes,
-                          max_len=max_len)
+                          max_len=max_len, min_len=min_len)
     _native.check(_native.lib.bmqcrc_crc32c_batch(
         arena.data_ptr(), arena.numel(), offsets.data_ptr(), lengths.data_ptr(),
         seeds.data_ptr() if seeds is not None else None, out.data_ptr(), n, ctypes.byref(o)))

@@ -389,13 +389,23 @@ uint64_t max_length(const uint32_t* lengths, uint64_t n)
     return m;
 }
 
+uint64_t min_length(const uint32_t* lengths, uint64_t n)
+{
+    uint32_t m = n ? UINT32_MAX : 0u;
+    for (uint64_t i = 0; i < n; ++i) {
+        m = std::min(m, lengths[i]);
+    }
+    return m;
+}
+
 // host_max_len: the longest message when the lengths were seen on the host, or
 // the caller's declared bound for device lengths (bmqcrc_opts.max_len: a
 // message over it is still exact, folded by its wave's second pass)
 // (host-buffer calls), UINT64_MAX when they live on the device.
 int run_batch(Ctx& c, uint32_t flags, uint32_t seg, const void* arena, uint64_t arena_bytes,
               const uint64_t* offsets, const uint32_t* lengths, const uint32_t* seeds,
-              uint32_t* out, uint64_t n, uint64_t host_max_len = UINT64_MAX)
+              uint32_t* out, uint64_t n, uint64_t host_max_len = UINT64_MAX,
+              uint64_t host_min_len = 0)
 {
     Workspace* w = c.w;
     BatchArgs a;
@@ -429,6 +439,15 @@ int run_batch(Ctx& c, uint32_t flags, uint32_t seg, const void* arena, uint64_t 
     }
     if (!a.whole && host_max_len <= a.seg_bytes && !(flags & BMQCRC_F_PLAN)) {
         a.spec = 1;  // known, not guessed: every message is one segment
+    } else if (!a.whole && host_min_len > 0 && host_max_len != UINT64_MAX &&
+               !(flags & BMQCRC_F_PLAN)) {
+        // every length in [min, max] has the same u segments, u dividing 64:
+        // the speculative uniform launch, known instead of guessed
+        const uint64_t u = (host_max_len - 1) / a.seg_bytes + 1;
+        if ((host_min_len - 1) / a.seg_bytes + 1 == u && u >= 2 && u <= 64 && 64 % u == 0 &&
+            (uint64_t)n * u <= 0xFFFFFF00ull) {
+            a.spec = (uint32_t)u;
+        }
     }
     a.arena = (const uint8_t*)arena;
     a.offsets = offsets;
@@ -477,11 +496,13 @@ int stage(Ctx& c, DevBuf& buf, const void* host, uint64_t bytes)
     return 0;
 }
 
-// declared_max: the caller's bound on every length of a device-resident batch
-// (bmqcrc_opts.max_len, 0 = none); host batches use the lengths they hold.
+// declared_max / declared_min: the caller's bounds on every length of a
+// device-resident batch (bmqcrc_opts.max_len / min_len, 0 = none); host
+// batches use the lengths they hold.
 int batch_one(int dev, void* user_stream, uint32_t flags, uint32_t seg, const void* arena,
               uint64_t arena_bytes, const uint64_t* offsets, const uint32_t* lengths,
-              const uint32_t* seeds, uint32_t* out, uint64_t n, uint32_t declared_max = 0)
+              const uint32_t* seeds, uint32_t* out, uint64_t n, uint32_t declared_max = 0,
+              uint32_t declared_min = 0)
 {
     Ctx c;
     int rc = open_ctx(dev, user_stream, &c);
@@ -493,7 +514,8 @@ int batch_one(int dev, void* user_stream, uint32_t flags, uint32_t seg, const vo
     const bool dev_ptrs = (flags & BMQCRC_F_DEVICE_PTRS) != 0;
     if (dev_ptrs) {
         if ((rc = run_batch(c, flags, seg, arena, arena_bytes, offsets, lengths, seeds, out, n,
-                            declared_max ? (uint64_t)declared_max : UINT64_MAX))) {
+                            declared_max ? (uint64_t)declared_max : UINT64_MAX,
+                            declared_max ? std::min(declared_min, declared_max) : 0u))) {
             return rc;
         }
         if (!(flags & BMQCRC_F_ASYNC)) {
@@ -509,7 +531,7 @@ int batch_one(int dev, void* user_stream, uint32_t flags, uint32_t seg, const vo
     if ((rc = run_batch(c, flags, seg, w->arena.p, arena_bytes, (const uint64_t*)w->offsets.p,
                         (const uint32_t*)w->lengths.p,
                         seeds ? (const uint32_t*)w->seeds.p : nullptr, (uint32_t*)w->out.p, n,
-                        max_length(lengths, n)))) {
+                        max_length(lengths, n), min_length(lengths, n)))) {
         return rc;
     }
     HIP_TRY(hipMemcpyAsync(out, w->out.p, 4 * n, hipMemcpyDeviceToHost, c.s));
@@ -646,7 +668,8 @@ int bmqcrc_crc32c_batch(const void* arena, uint64_t arena_bytes, const uint64_t*
                                          o.devices, (int)o.ndevices, seg);
     }
     return batch_one(dev, o.stream, o.flags, seg, arena, arena_bytes, offsets, lengths, seeds,
-                     out, n, (o.flags & BMQCRC_F_DEVICE_PTRS) ? o.max_len : 0u);
+                     out, n, (o.flags & BMQCRC_F_DEVICE_PTRS) ? o.max_len : 0u,
+                     (o.flags & BMQCRC_F_DEVICE_PTRS) ? o.min_len : 0u);
 }
 
 int bmqcrc_crc32c_verify(const void* arena, uint64_t arena_bytes, const uint64_t* offsets,

@@ -93,6 +93,12 @@ typedef struct bmqcrc_opts {
      * it in a second pass), only slower.  BMQCRC_F_PLAN takes precedence.
      * Callers built against ABI <= 2.3 (smaller struct_size) get 0. */
     uint32_t max_len;
+    /* ABI 2.4.  With max_len: the caller's lower bound on every lengths[i]
+     * (0 = none).  When every length in [min_len, max_len] has the same u
+     * segments and u divides 64 (1k x 4 KiB at 256-byte segments: u = 16),
+     * the batch is likewise one launch (the speculative uniform form, known
+     * instead of guessed); a message outside the range stays exact. */
+    uint32_t min_len;
 } bmqcrc_opts;
 
 /* ---- scalar (host CPU) -------------------------------------------------- */

@@ -64,13 +64,13 @@ def test_opts_layout_matches_the_header(tmp_path):
     from blazingmq_amd import _native as N
     src = tmp_path / "opts.c"
     src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "bmqcrc.h"\n'
-                   'int main(void) { printf("%zu %zu %zu %zu\\n", sizeof(bmqcrc_opts), '
+                   'int main(void) { printf("%zu %zu %zu %zu %zu\\n", sizeof(bmqcrc_opts), '
                    'offsetof(bmqcrc_opts, ndevices), offsetof(bmqcrc_opts, devices), '
-                   'offsetof(bmqcrc_opts, max_len)); return 0; }\n')
+                   'offsetof(bmqcrc_opts, max_len), offsetof(bmqcrc_opts, min_len)); return 0; }\n')
     exe = tmp_path / "opts"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)],
                    check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True,
                                           check=True).stdout.split()]
     assert got == [ctypes.sizeof(N.Opts), N.Opts.ndevices.offset, N.Opts.devices.offset,
-                   N.Opts.max_len.offset]
+                   N.Opts.max_len.offset, N.Opts.min_len.offset]

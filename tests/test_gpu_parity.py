@@ -640,6 +640,17 @@ def test_declared_max_len_single_launch(cuda):
     assert run(ragged(), "bound over a segment", max_len=1 << 20)["kernels"] >= 2
     # BMQCRC_F_PLAN takes precedence
     assert run(short(), "plan wins", max_len=256, plan=True)["kernels"] >= 2
+    # a declared range of one segment count u (u | 64): the uniform single
+    # launch (configs[0]'s shape, 1,000 x 4 KiB), then the range broken
+    assert run(ragged()[:1000], "small ragged")["kernels"] >= 2
+    ll = run(np.full(1000, 4096), "declared uniform range", max_len=4096, min_len=4096)
+    u = (4096 - 1) // ll["seg_bytes"] + 1
+    if 2 <= u <= 64 and 64 % u == 0:
+        assert ll["kernels"] == 1 and ll["spec"] == u, ll
+    broken = np.full(1000, 4096)
+    broken[[0, 77, 999]] = [5000, 0, 100]
+    run(broken, "declared uniform range broken", max_len=4096, min_len=4096)
+    run(rng.integers(3900, 4097, size=1000), "range inside one u", max_len=4096, min_len=3900)
 
 
 def test_ranks_shard_a_batch_on_the_gpu(cuda):
