@@ -113,6 +113,9 @@ def parse():
                    help="end-to-end mode: H2D from pinned host + CRC + D2H (for DESIGN.md)")
     p.add_argument("--no-strong-scaling", action="store_true",
                    help="N > 1: skip the strong-scaled Zipf object")
+    p.add_argument("--plan-wait-us", type=int, default=None,
+                   help="bmqcrc_plan_wait limit for this run (default: the library's 1000 us; "
+                        "0 gives every ragged batch's size-class map up: the fallback's cost)")
     p.add_argument("--launch-check", action="store_true",
                    help="test hook: start the ranks, rendezvous over gloo and print the "
                         "world as rank 0 sees it, without touching a GPU")
@@ -143,12 +146,23 @@ def host_threads():
         return min(os.cpu_count() or 1, 16)
 
 
+# The reference's published default-CRC32C time per buffer (ns), 64-bit
+# hardware-accelerated build (bmqp_crc32c.h:116,119,122,127,129), measured by
+# its tight loop of 100,000 calls on one buffer (bmqp_crc32c.t.cpp:1116-1120).
+REF_PUBLISHED_NS = {256: (30, "bmqp_crc32c.h:116"), 1024: (45, "bmqp_crc32c.h:119"),
+                    4096: (176, "bmqp_crc32c.h:122"), 65536: (2858, "bmqp_crc32c.h:127"),
+                    1 << 20: (50937, "bmqp_crc32c.h:129")}
+
+
 def cpu_baseline(lens_np, seed, seconds):
     """Reference-equivalent CPU CRC32C (oracle, SSE4.2 3-way; BDE 4.39 is not
     available offline) on a bounded sample (first ~256 MiB of messages) of the
-    same synthetic workload: single thread (the reference's own methodology,
-    bmqp_crc32c.t.cpp:1116-1120) and this GPU's share of the host's threads
-    (the test5 pattern, one thread per core over message slices)."""
+    same synthetic workload.  Three legs, each warm (one untimed pass) and
+    timed for >= 0.5 s: the batch on one thread, the batch on this GPU's share
+    of the host's threads (created once, before the clock; the test5 pattern,
+    one thread per byte-balanced message slice), and the reference's own
+    benchmark loop (bmqp_crc32c.t.cpp:1116-1120: one message CRC'd up to
+    100,000 times) for messages up to 1 MiB, beside its published figure."""
     import numpy as np
     import oracle
     threads = host_threads()
@@ -160,29 +174,47 @@ def cpu_baseline(lens_np, seed, seconds):
         offs[1:] = csum[:n - 1]
     nbytes = int(lens.sum(dtype=np.uint64))
     arena = oracle.fill_payload(0, nbytes, seed)
-    t1, _ = oracle.time_batch(arena, offs, lens, 1, "hw", 1)          # single thread
-    t, _ = oracle.time_batch(arena, offs, lens, threads, "hw", 1)      # calibrate
-    reps = max(1, int(seconds / max(t, 1e-6)))
-    t, _ = oracle.time_batch(arena, offs, lens, threads, "hw", reps)
+    t1, reps1 = oracle.time_batch_for(arena, offs, lens, 1, "hw", 0.5)
+    t, reps = oracle.time_batch_for(arena, offs, lens, threads, "hw", max(0.5, seconds))
     gib = nbytes / 2**30
-    return {
+    res = {
         "value": round(gib * reps / t, 3),
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
-        "single_thread_value": round(gib / t1, 3),
+        "single_thread_value": round(gib * reps1 / t1, 3),
         "host_threads": os.cpu_count(),
         "not_measured": "nproc/8 (%d threads, one GPU's share of an 8-GPU node) and all %d "
                         "threads: a one-GPU job on this pool may use %d threads "
                         "(OMP_NUM_THREADS); the rest of the shared host is not ours to load"
                         % ((os.cpu_count() or 8) // 8, os.cpu_count() or 0, threads),
-        "sample": "first %d msgs (%.0f MiB) of the same synthetic batch, %d passes on %d "
-                  "threads (this GPU's share of the host: OMP_NUM_THREADS, 16 per GPU on the "
-                  "pool; the whole host is not ours to load); SSE4.2 crc32q 3-way interleaved "
-                  "(bdlde::Crc32c default analogue, oracle/crc32c_oracle.c); single-thread "
-                  "%.2f GiB/s; host %s, nproc %d"
-                  % (n, gib * 1024, reps, threads, gib / t1, cpu_model(), os.cpu_count()),
+        "sample": "first %d msgs (%.0f MiB) of the same synthetic batch; %d threads (this "
+                  "GPU's share of the host: OMP_NUM_THREADS, 16 per GPU on the pool), created "
+                  "once before the clock, %d warm passes (%.2f s); single thread %d warm passes "
+                  "(%.2f s) = %.2f GiB/s; SSE4.2 crc32q 3-way interleaved (bdlde::Crc32c "
+                  "default analogue, oracle/crc32c_oracle.c); host %s, nproc %d"
+                  % (n, gib * 1024, threads, reps, t, reps1, t1, gib * reps1 / t1, cpu_model(),
+                     os.cpu_count()),
     }
+    size = int(lens_np[0]) if lens_np.size else 0
+    if 0 < size <= (1 << 20) and bool(np.all(lens == size)):
+        buf = arena[:size]
+        iters = 100000
+        tr = oracle.time_repeat(buf, 1000)
+        iters = int(min(100000, max(1000, 0.5 / max(tr / 1000, 1e-9))))
+        tr = oracle.time_repeat(buf, iters)
+        ref = {"ns_per_msg": round(1e9 * tr / iters, 1), "msg_bytes": size, "iters": iters,
+               "GiBps": round(size * iters / tr / 2**30, 3),
+               "method": "the reference's loop: one buffer CRC'd `iters` times on one thread "
+                         "(bmqp_crc32c.t.cpp:1116-1120), oracle SSE4.2 3-way",
+               "batch_ns_per_msg_1_thread": round(1e9 * t1 / reps1 / n, 1)}
+        if size in REF_PUBLISHED_NS:
+            ns, where = REF_PUBLISHED_NS[size]
+            ref.update({"reference_published_ns": ns, "reference_published_at": where,
+                        "reference_published_host": "the reference's own (unnamed) 64-bit "
+                                                    "build host"})
+        res["reference_loop"] = ref
+    return res
 
 
 CPU_VARIANTS = {"hw": "SSE4.2 crc32q 3-way interleaved (bdlde::Crc32c::calculate default)",
@@ -539,6 +571,8 @@ def main():
         step(False)
     torch.cuda.synchronize(dev)
     bmq.kernel_timing(local, stream)  # reset
+    wait_us = 1000 if args.plan_wait_us is None else args.plan_wait_us
+    voided0 = bmq.plan_wait(local, stream, wait_us)  # given-up planner maps so far
 
     if world > 1:
         dist.barrier()
@@ -552,6 +586,7 @@ def main():
         dist.barrier()
     elapsed = t1 - t0
     launch = bmq.last_launch(local, stream)  # the steady-state step's launch plan
+    voided1 = bmq.plan_wait(local, stream, wait_us)
     # The same K steps with the shape prediction off (BMQCRC_F_PLAN): what a
     # caller whose batch shapes alternate on one stream pays per batch.
     if world > 1:
@@ -563,6 +598,7 @@ def main():
     torch.cuda.synchronize(dev)
     planned = time.perf_counter() - t0
     planned_launch = bmq.last_launch(local, stream)
+    voided2 = bmq.plan_wait(local, stream, wait_us)
     # ... and with the prediction dropped before every step but the batch's
     # length bounds declared (bmqcrc_opts.max_len / min_len, ABI 2.4): what a
     # caller that knows its message sizes pays when shapes alternate.
@@ -593,7 +629,11 @@ def main():
     del arena  # the strong-scaling leg below needs the memory
     bytes_all = total_bytes
     kern_max = kern_ms / max(kern_cnt, 1)
+    plan_voided = [voided1 - voided0, voided2 - voided1]
     if world > 1:
+        vt = torch.tensor(plan_voided, dtype=torch.int64)
+        dist.all_reduce(vt)
+        plan_voided = [int(vt[0]), int(vt[1])]
         tt = torch.tensor([elapsed, kern_max, planned, declared], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed, kern_max, planned, declared = (float(tt[0]), float(tt[1]), float(tt[2]),
@@ -663,6 +703,11 @@ def main():
             "planned_ms_per_step": round(1e3 * planned / args.steps, 4),
             "planned_value": round(bytes_all / 2**30 * args.steps / planned, 2),
             "planned_kernels_per_step": planned_launch["kernels"],
+            # single-pass planner launches (all ranks) whose size-class map was
+            # given up, in the K timed steps and in the K planned steps
+            "plan_voided": plan_voided[0],
+            "planned_plan_voided": plan_voided[1],
+            "plan_wait_us": wait_us,
         }
         # the bounds buy one launch only when every length in them has the
         # same u segments, u dividing 64; otherwise an in-flight batch may

@@ -151,6 +151,11 @@ struct Workspace {
 
 struct DeviceState {
     int num_cus = 0;
+    // k_plan_map blocks the device holds at once (occupancy x CUs, at most
+    // kPlanMaxBlocks): its grid never exceeds this, so on an idle GPU every
+    // block is resident for the grid-wide meeting (a partitioned or smaller
+    // part gets fewer, fuller blocks instead of a wait that must give up)
+    uint32_t plan_resident = kPlanMaxBlocks;
 };
 
 std::mutex g_mu;
@@ -193,6 +198,13 @@ int device_state(int dev, DeviceState** st)
             return fail(BMQCRC_ENODEV, std::string("device is ") + prop.gcnArchName +
                                            ", this library is built for gfx950 (MI355X) only");
         }
+        HIP_TRY(hipSetDevice(dev));
+        int per = 0;
+        if (bmqcrc_plan_map_occupancy(&per) != 0 || per <= 0) {
+            return fail(BMQCRC_EIO, "k_plan_map occupancy query failed");
+        }
+        s.plan_resident = (uint32_t)std::min<uint64_t>(
+            (uint64_t)per * (uint64_t)std::max(prop.multiProcessorCount, 1), kPlanMaxBlocks);
         s.num_cus = prop.multiProcessorCount;
     }
     *st = &s;
@@ -222,10 +234,12 @@ uint64_t max_segs_for(uint64_t n, uint64_t arena_bytes, uint32_t seg)
 // Fewer, fuller blocks -- at least 8 tiles each, so that the 1/8 Zipf shard
 // takes the single-pass planner -- traced 36.8 against 26.3 us there,
 // profiles/r03/ab/planner_block_sizing/.)
-static void split_ranges(uint64_t items, uint64_t* per, uint32_t* blocks)
+static void split_ranges(uint64_t items, uint64_t* per, uint32_t* blocks,
+                         uint32_t max_blocks = kPlanMaxBlocks)
 {
     const uint64_t tiles = std::max<uint64_t>((items + kPlanBlock - 1) / kPlanBlock, 1);
-    const uint64_t nb = std::min<uint64_t>(tiles, kPlanMaxBlocks);
+    const uint64_t nb = std::min<uint64_t>(
+        tiles, std::max<uint32_t>(1u, std::min<uint32_t>(max_blocks, kPlanMaxBlocks)));
     uint64_t tiles_per = (tiles + nb - 1) / nb;
     if (kTuneBits & 512u) {  // A/B: whole planner tiles (kPlanV x kPlanBlock) per block
         tiles_per = (tiles_per + kPlanV - 1) / kPlanV * kPlanV;
@@ -235,10 +249,12 @@ static void split_ranges(uint64_t items, uint64_t* per, uint32_t* blocks)
 }
 
 int plan_ws(Workspace* w, hipStream_t s, uint64_t n, uint64_t arena_bytes, uint32_t seg,
-            BatchArgs* a, int num_cus = 256)
+            BatchArgs* a, const DeviceState& st)
 {
+    const int num_cus = st.num_cus;
     const uint64_t max_segs = max_segs_for(n, arena_bytes, seg);
-    split_ranges(n, &a->per_msg, &a->nblocks);
+    // k_plan_map's blocks meet grid-wide: never more than the GPU holds
+    split_ranges(n, &a->per_msg, &a->nblocks, st.plan_resident);
     int rc;
     if ((rc = w->seg_first.ensure(4 * std::max<uint64_t>(n, 1))) ||
         (rc = w->block_sum.ensure(12ull * kPlanMaxBlocks)) ||
@@ -418,7 +434,7 @@ int run_batch(Ctx& c, uint32_t flags, uint32_t seg, const void* arena, uint64_t 
     if (flags & BMQCRC_F_WHOLE_MESSAGES) {
         a.whole = 1;  // identity map over messages: no planner workspace
         a.max_segs = n;
-    } else if ((rc = plan_ws(w, c.s, n, arena_bytes, seg, &a, c.st->num_cus))) {
+    } else if ((rc = plan_ws(w, c.s, n, arena_bytes, seg, &a, *c.st))) {
         return rc;
     } else if (!(kTuneBits & 16u) && !(flags & BMQCRC_F_PLAN)) {
         const uint32_t hint = __atomic_load_n(w->hint_host, __ATOMIC_RELAXED);
@@ -544,8 +560,11 @@ int parse_opts(const bmqcrc_opts* opts, bmqcrc_opts* o, uint32_t* seg, int* dev)
     memset(o, 0, sizeof(*o));
     o->device = -1;
     if (opts) {
-        memcpy(o, opts,
-               std::min<size_t>(sizeof(*o), opts->struct_size ? opts->struct_size : sizeof(*o)));
+        // struct_size 0 reads only the ABI 2.0 fields: a caller that never set
+        // it may be built against any earlier, shorter layout
+        const size_t given = opts->struct_size ? opts->struct_size : offsetof(bmqcrc_opts, ndevices);
+        memcpy(o, opts, std::min<size_t>(sizeof(*o), given));
+        o->struct_size = sizeof(*o);
     }
     *seg = o->seg_bytes;
     const uint32_t known = BMQCRC_F_DEVICE_PTRS | BMQCRC_F_ASYNC | BMQCRC_F_TIME_KERNEL |
@@ -1493,9 +1512,9 @@ int bmqcrc_reserve(int device, void* stream, uint64_t n_msgs, uint64_t arena_byt
     Workspace* w = workspace(dev, stream);
     std::lock_guard<std::mutex> g(w->mu);
     BatchArgs a;
-    uint32_t per_cu;
-    auto_shape(n_msgs, arena_bytes, st->num_cus, &seg_bytes, &per_cu);  // as the batch call will
-    return plan_ws(w, (hipStream_t)stream, n_msgs, arena_bytes, seg_bytes, &a);
+    memset(&a, 0, sizeof(a));
+    auto_shape(n_msgs, arena_bytes, st->num_cus, &seg_bytes, &a.blocks_per_cu);  // as the batch call will
+    return plan_ws(w, (hipStream_t)stream, n_msgs, arena_bytes, seg_bytes, &a, *st);
 }
 
 int bmqcrc_fill_synthetic(void* dev_dst, uint64_t nbytes, uint64_t seed, uint64_t begin,
@@ -1696,7 +1715,7 @@ uint64_t bmqcrc_host_fallbacks(int32_t* last_rc)
 
 uint32_t bmqcrc_version(void)
 {
-    return (2u << 16) | 4u;
+    return (2u << 16) | 5u;
 }
 
 }  // extern "C"

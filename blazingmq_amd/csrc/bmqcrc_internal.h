@@ -86,7 +86,7 @@ struct BatchArgs {
     // guess was wrong.
     uint32_t spec;
     // Single-pass planner (k_plan_map): [2] the epoch of a launch whose map
-    // was given up (k_fold then folds every message whole), [3] how many
+    // was given up (k_fold then searches seg_first), [3] how many
     // launches gave theirs up, [kSyncFlags + b] block b's arrival flag (the
     // epoch of the launch it last arrived in), then kPlanMaxBlocks x
     // (kBuckets + 3) epoch-tagged words the blocks exchange.  Zeroed once
@@ -128,6 +128,8 @@ constexpr uint32_t kHintIdentity = 3;  // one segment per message
 // Launchers (crc32c_kernels.hip).  All asynchronous on `stream`.
 extern "C" __attribute__((visibility("hidden"))) int bmqcrc_launch_batch(const bmqcrc::BatchArgs* a, void* stream, int num_cus,
                                    void* ev_start, void* ev_stop);
+// k_plan_map blocks one CU holds at once (hipOccupancyMaxActiveBlocksPerMultiprocessor).
+extern "C" __attribute__((visibility("hidden"))) int bmqcrc_plan_map_occupancy(int* blocks_per_cu);
 extern "C" __attribute__((visibility("hidden"))) int bmqcrc_launch_compare(const uint32_t* got, const uint32_t* expected, uint64_t n,
                                      uint32_t* bad_count, uint32_t* bad_idx, uint32_t bad_cap,
                                      void* stream);

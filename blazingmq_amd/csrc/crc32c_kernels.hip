@@ -546,6 +546,38 @@ __device__ uint32_t find_msg(const BatchArgs& a, const PlanLds* pl, uint32_t g)
     return (uint32_t)lo;
 }
 
+// The same for a whole group (lane l holds segment s0 + l, s0 = 64 g): one
+// wave-uniform search for s0's message m0, then the first segments of
+// messages m0 .. m0 + 63 (one coalesced load) and a 6-step search in
+// registers.  A lane past the window (the group spans more than 64
+// messages: empty ones in between) searches on its own.  Returns the
+// message; *first = its first segment.  All 64 lanes must be active.
+__device__ __forceinline__ uint32_t find_msg_group(const BatchArgs& a, const PlanLds* pl,
+                                                   uint32_t seg, bool valid, uint32_t* first)
+{
+    const uint32_t lane = (uint32_t)(threadIdx.x & 63);
+    const uint32_t s0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(seg - lane));
+    const uint32_t m0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)find_msg(a, pl, s0));
+    const uint64_t mj = (uint64_t)m0 + lane;
+    const uint32_t w = mj < a.n ? seg_first_g(a, pl, mj) : 0xffffffffu;
+    const uint32_t wn = (lane == 63u && mj + 1u < a.n) ? seg_first_g(a, pl, mj + 1u) : 0xffffffffu;
+    uint32_t j = 0;  // largest j with w_j <= seg (w_0 <= s0 <= seg)
+#pragma unroll
+    for (uint32_t st = 32; st; st >>= 1) {
+        const uint32_t c = (uint32_t)__shfl((int)w, (int)(j + st));
+        j = c <= seg ? j + st : j;
+    }
+    uint32_t msg = m0 + j;
+    uint32_t f = (uint32_t)__shfl((int)w, (int)j);
+    const uint32_t w64 = (uint32_t)__builtin_amdgcn_readlane((int)wn, 63);
+    if (valid && j == 63u && w64 <= seg) {
+        msg = find_msg(a, pl, seg);
+        f = seg_first_g(a, pl, msg);
+    }
+    *first = f;
+    return msg;
+}
+
 // Block-wide exclusive scan of v over blockDim.x threads (a multiple of 64,
 // at most 1024); returns the block total.  wsum: 33 words of LDS.
 __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* excl, uint32_t* wsum)
@@ -725,19 +757,29 @@ __device__ __forceinline__ SegRef map_segment(const BatchArgs& a, const PlanLds*
                                               uint32_t uni, uint32_t sorted)
 {
     SegRef r = {0u, 0u};
+    if (!identity && !uni && !sorted) {
+        // no map (skipped, given up or past seginfo): search seg_first, one
+        // search per group (wave-uniform branch: every lane takes part)
+        if (__ballot(valid) != 0) {
+            uint32_t f = 0;
+            const uint32_t m = find_msg_group(a, pl, seg, valid, &f);
+            if (valid) {
+                r.msg = m;
+                r.k = seg - f;
+            }
+        }
+        return r;
+    }
     if (valid) {
         if (identity) {
             r.msg = seg;
         } else if (uni) {
             r.msg = seg / uni;
             r.k = seg - r.msg * uni;
-        } else if (sorted) {
-            // the raw entry and its group's firstk (resolved in fetch_desc)
+        } else {
+            // sorted: the raw entry and its group's firstk (resolved in fetch_desc)
             r.msg = a.seginfo[seg];
             r.k = a.firstk[(uint32_t)__builtin_amdgcn_readfirstlane((int)seg) >> 6];
-        } else {
-            r.msg = find_msg(a, pl, seg);  // no map (skipped or overflow): binary search
-            r.k = seg - seg_first_g(a, pl, r.msg);
         }
     }
     return r;
@@ -861,12 +903,12 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     } else {
         __syncthreads();
     }
-    // more segments than 32-bit indices hold, or k_plan_map gave its map up
-    // (it then writes no seg_first to search): every message in one lane
-    const uint32_t wholef = whole | pt.overflow | map_void;
+    // more segments than 32-bit indices hold: every message in one lane.  A
+    // map k_plan_map gave up is not used; its seg_first is (binary search).
+    const uint32_t wholef = whole | pt.overflow;
     const uint32_t hint_identity = pt.identity && !pt.overflow;
     const uint32_t hint_uni = pt.uni;
-    if (pt.overflow || map_void) {
+    if (pt.overflow) {
         pt.identity = 1u;
         pt.uni = 0u;
         pt.total = (uint32_t)a.n;
@@ -875,7 +917,7 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     const uint32_t identity = pt.identity;
     const uint32_t uni = pt.uni;
     // the size-class order exists only if the histogram and k_plan_sort ran
-    // (and seginfo could hold every segment)
+    // (and seginfo could hold every segment, and k_plan_map kept its map)
     const uint32_t sorted =
         (wholef || !a.map_planned || identity || uni || total > a.max_segs || map_void) ? 0u : 1u;
     const uint32_t ngroups = (total + 63u) / 64u;
@@ -1755,15 +1797,16 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_sort(BatchArgs a)
 // waves then draw a binomial mix of 16-round and 1-round groups, and Zipf's
 // k_fold ran 7 % slower, profiles/r03/ab/ab1_*.jsonl.)
 //
-// Safety of the wait: a grid of <= kPlanMaxBlocks blocks normally fits the
-// GPU at once, but nothing guarantees it (other streams, other processes).
-// A block that has waited map_wait_ticks (1 ms by default, bmqcrc_plan_wait)
+// Safety of the wait: the host sizes the grid to what the GPU holds at once
+// (occupancy x CUs), but nothing guarantees residency (other streams, other
+// processes).  A block that has waited map_wait_ticks (bmqcrc_plan_wait)
 // without seeing every arrival marks the map invalid for this launch
-// (plan_sync[2] = epoch, plan_sync[3] counts such launches) and leaves;
-// k_fold then ignores the planner's output and folds every message whole in
-// one lane (the schedule of BMQCRC_F_WHOLE_MESSAGES: exact, slower).  With
-// the map in use seg_first is not written.  Arrival flags carry the launch's
-// epoch, so nothing needs resetting between launches.
+// (plan_sync[2] = epoch, plan_sync[3] counts such launches) and leaves; a
+// block that finds the map already given up leaves at once.  Every block
+// writes seg_first and the out[] initialisation in every path, so k_fold
+// then maps segments by searching seg_first (message order instead of
+// size-class order: exact, somewhat slower).  Arrival flags carry the
+// launch's epoch, so nothing needs resetting between launches.
 #ifndef BMQCRC_MAP_REG_TILES
 #define BMQCRC_MAP_REG_TILES 4
 #endif
@@ -2005,9 +2048,20 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
         const uint64_t t0 = wall_clock64();
         uint32_t ok = 1u;
         static_assert(kPlanMaxBlocks <= 4 * 64, "four flags per lane");
-        while (true) {
+        // a zero limit gives the map up before the first poll (the test hook
+        // of bmqcrc_plan_wait(0): every such launch takes the fallback)
+        bool waiting = a.map_wait_ticks != 0;
+        if (!waiting) {
+            ok = 0u;
+            if (lane == 0) {
+                give_up();
+            }
+        }
+        while (waiting) {
             // all four loads in flight at once (a short-circuit chain made
-            // them four round trips per poll)
+            // them four round trips per poll), plus the launch's give-up word:
+            // a block arriving after another gave the map up leaves at once
+            // instead of waiting out its own limit
             unsigned long long f[4];
 #pragma unroll
             for (uint32_t k = 0; k < 4; ++k) {
@@ -2016,8 +2070,14 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
                                                   __HIP_MEMORY_SCOPE_AGENT)
                               : (unsigned long long)ep;
             }
+            const unsigned long long gone =
+                __hip_atomic_load(&sync[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const bool mine = f[0] == ep && f[1] == ep && f[2] == ep && f[3] == ep;
             if (__ballot(!mine) == 0) {
+                break;
+            }
+            if (gone == (unsigned long long)ep) {
+                ok = 0u;  // another block gave this launch's map up
                 break;
             }
             if (wall_clock64() - t0 >= a.map_wait_ticks) {
@@ -2036,11 +2096,10 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
     }
     __syncthreads();
     PLAN_STAMP(4)
-    if (!go) {
-        // the map is given up: k_fold folds every message whole in one lane
-        // and stores it plainly (no seg_first, no out[] initialisation)
-        return;
-    }
+    // false: no map for k_fold (given up, or a closed form / past capacity
+    // below); it then searches seg_first, and multi-segment messages
+    // XOR-combine into out[] -- both written by deferred() in every path
+    bool map = go != 0;
     // Batch shape and size from every block's words (closed-form batches
     // and those past seginfo's capacity or 32-bit indices need no map), and
     // this block's slice of every class (k_plan_sort's class-major order):
@@ -2052,7 +2111,7 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
     const uint32_t cw = threadIdx.x >> 6;
     const uint32_t j = threadIdx.x;
     uint32_t u0 = 0;
-    {
+    if (map) {  // block-uniform (go is in LDS)
         const uint64_t t1 = wall_clock64();
         auto tagged = [&](const unsigned long long* p, uint32_t& val, bool& stale) {
             const unsigned long long x = __hip_atomic_load(p, __ATOMIC_RELAXED,
@@ -2119,13 +2178,13 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
                 if (threadIdx.x == 0) {
                     give_up();
                 }
-                return;
+                map = false;
+                break;
             }
             __syncthreads();  // part[] read by all before the next round
         }
     }
-    bool map = true;
-    {
+    if (map) {
         uint32_t flags = 0;
         unsigned long long all = 0;
 #pragma unroll
@@ -2150,11 +2209,12 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
             run[threadIdx.x] = acc + part[1][0][threadIdx.x];
         }
     }
-    // seg_first only without a map (k_fold then uses closed forms or
-    // searches it).  With the map it is never read: should another block
-    // give the map up after this one saw every arrival (its timer ran out
-    // between two polls), k_fold folds every message whole instead.
-    deferred(!map);
+    // seg_first in every path: should another block give the map up after
+    // this one saw every arrival (its timer ran out between two polls),
+    // k_fold searches seg_first for every segment of the batch (16 MB of
+    // stores on Zipf 4M; round 3 skipped them and fell back to one lane per
+    // message, a cliff of up to the longest message per wave).
+    deferred(true);
     PLAN_STAMP(5)
     if (!map) {
         return;
@@ -2482,6 +2542,17 @@ extern "C" int bmqcrc_launch_batch(const BatchArgs* a, void* stream, int num_cus
         (void)hipEventRecord((hipEvent_t)ev_stop, s);
     }
     return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" int bmqcrc_plan_map_occupancy(int* blocks_per_cu)
+{
+    int per = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&k_plan_map),
+                                                     kPlanBlock, 0) != hipSuccess) {
+        return -5;
+    }
+    *blocks_per_cu = per;
+    return 0;
 }
 
 #if BMQCRC_PLAN_DIAG >= 3

@@ -62,7 +62,8 @@ extern "C" {
 #define BMQCRC_F_PLAN 0x10u
 
 typedef struct bmqcrc_opts {
-    uint32_t struct_size; /* sizeof(bmqcrc_opts) */
+    uint32_t struct_size; /* sizeof(bmqcrc_opts); 0 reads the ABI 2.0 fields only (device,
+                             stream, flags, seg_bytes): set it to use anything later */
     int32_t device;       /* HIP device ordinal; -1 = current device */
     void* stream;         /* hipStream_t; NULL = that device's default (null) stream */
     uint32_t flags;       /* BMQCRC_F_* */
@@ -93,7 +94,7 @@ typedef struct bmqcrc_opts {
      * it in a second pass), only slower.  BMQCRC_F_PLAN takes precedence.
      * Callers built against ABI <= 2.3 (smaller struct_size) get 0. */
     uint32_t max_len;
-    /* ABI 2.4.  With max_len: the caller's lower bound on every lengths[i]
+    /* ABI 2.5.  With max_len: the caller's lower bound on every lengths[i]
      * (0 = none).  When every length in [min_len, max_len] has the same u
      * segments and u divides 64 (1k x 4 KiB at 256-byte segments: u = 16),
      * the batch is likewise one launch (the speculative uniform form, known
@@ -204,13 +205,16 @@ int bmqcrc_forget_shape(int device, void* stream);
 /* ABI 2.3.  Longest time (microseconds) the blocks of the single-pass
  * planner (ragged batches) wait for each other on (device, stream) before
  * giving up the size-class map of that batch; default 1000.  The planner's
- * blocks meet once, grid-wide; when the GPU cannot run them all at once
- * (other streams or processes hold the CUs) a block that waited this long
- * leaves, and the fold then folds every message of that batch whole in one
- * lane -- results are exact either way, only slower.  0 gives every map up at once (a test hook
- * for that path).  *voided (may be NULL) receives how many planned batches on
- * (device, stream) gave up their map so far; asking for it waits for the
- * work already enqueued on that stream. */
+ * blocks meet once, grid-wide, and its grid never exceeds what the device
+ * holds at once; when the GPU still cannot run them all together (other
+ * streams or processes hold the CUs) a block that waited this long gives the
+ * map up, blocks that find it given up leave at once, and the fold maps that
+ * batch's segments by searching the per-message segment offsets instead of
+ * the size-class order (ABI 2.5; before, one lane per message) -- results are
+ * exact either way, only slower.  0 gives every map up before the first poll
+ * (a test hook for that path).  *voided (may be NULL) receives how many
+ * planned batches on (device, stream) gave up their map so far; asking for it
+ * waits for the work already enqueued on that stream. */
 int bmqcrc_plan_wait(int device, void* stream, uint64_t wait_us, uint64_t* voided);
 
 /* Zero-copy input: page-lock `bytes` of ordinary host memory at `host` and map
@@ -240,7 +244,7 @@ const char* bmqcrc_last_error(void);
 void bmqcrc_note_host_fallback(int32_t rc);
 uint64_t bmqcrc_host_fallbacks(int32_t* last_rc);
 
-/* ABI version: (major << 16) | minor (2.4). */
+/* ABI version: (major << 16) | minor (2.5). */
 uint32_t bmqcrc_version(void);
 
 #ifdef __cplusplus

@@ -41,6 +41,9 @@ def lib():
         L.oracle_time_batch.restype = ctypes.c_double
         L.oracle_time_batch.argtypes = [vp, vp, vp, vp, vp, ctypes.c_size_t, ctypes.c_int,
                                         ctypes.c_int, ctypes.c_int]
+        L.oracle_time_repeat.restype = ctypes.c_double
+        L.oracle_time_repeat.argtypes = [vp, u32, ctypes.c_int, ctypes.c_int,
+                                         ctypes.POINTER(u32)]
         L.oracle_fill_payload.restype = None
         L.oracle_fill_payload.argtypes = [vp, u64, u64, u64]
         L.oracle_have_sse42.restype = ctypes.c_int
@@ -95,6 +98,27 @@ def time_batch(arena, offsets, lengths, nthreads, variant="hw", reps=1):
     t = lib().oracle_time_batch(a.ctypes.data, off.ctypes.data, ln.ctypes.data, None,
                                 out.ctypes.data, off.size, nthreads, VARIANTS[variant], reps)
     return t, out
+
+
+def time_batch_for(arena, offsets, lengths, nthreads, variant="hw", seconds=0.5):
+    """Passes over the batch on `nthreads` threads (created once, one untimed
+    warm-up pass) until about `seconds` of timed work: (seconds, passes)."""
+    t, _ = time_batch(arena, offsets, lengths, nthreads, variant, 1)
+    reps = 1
+    while t < seconds:  # at most a few rounds: each aims 20 % past the target
+        reps = max(reps + 1, int(1.2 * seconds * reps / max(t, 1e-7)))
+        t, _ = time_batch(arena, offsets, lengths, nthreads, variant, reps)
+    return t, reps
+
+
+def time_repeat(buf, iters, variant="hw"):
+    """The reference's benchmark loop (bmqp_crc32c.t.cpp:1116-1120): one
+    buffer CRC'd `iters` times on one thread after an untimed call.  Returns
+    seconds."""
+    a, p = _buf(buf)
+    c = ctypes.c_uint32()
+    return lib().oracle_time_repeat(p, a.size if len(buf) else 0, iters, VARIANTS[variant],
+                                    ctypes.byref(c))
 
 
 def fill_payload(begin, nbytes, seed):

@@ -306,27 +306,16 @@ static void *batch_worker(void *arg)
     return NULL;
 }
 
-/* CRC every message of a batch on `nthreads` host threads, messages split
- * into contiguous byte-balanced slices (the reference's test5 pattern,
- * bmqp_crc32c.t.cpp:705-760).  variant: 0 hw 3-way, 1 hw serial, 2 slicing-by-8,
- * 3 bitwise.  Returns 0. */
-int oracle_crc32c_batch(const uint8_t *arena, const uint64_t *off, const uint32_t *len,
-                        const uint32_t *seed, uint32_t *out, size_t n, int nthreads, int variant)
+/* Contiguous byte-balanced slices of a batch, one per thread (the
+ * reference's test5 pattern, bmqp_crc32c.t.cpp:705-760). */
+static void split_jobs(struct batch_job *jobs, int nthreads, const uint8_t *arena,
+                       const uint64_t *off, const uint32_t *len, const uint32_t *seed,
+                       uint32_t *out, size_t n, int variant)
 {
-    enum { MAXT = 256 };
-    if (nthreads < 1) {
-        nthreads = 1;
-    }
-    if (nthreads > MAXT) {
-        nthreads = MAXT;
-    }
-    pthread_once(&g_tab_once, init_tables);
     uint64_t total = 0;
     for (size_t i = 0; i < n; ++i) {
         total += len[i];
     }
-    struct batch_job jobs[MAXT];
-    pthread_t th[MAXT];
     size_t i = 0;
     uint64_t acc = 0;
     for (int t = 0; t < nthreads; ++t) {
@@ -344,6 +333,26 @@ int oracle_crc32c_batch(const uint8_t *arena, const uint64_t *off, const uint32_
         }
         jobs[t].hi = i;
     }
+}
+
+enum { MAXT = 256 };
+
+static int clamp_threads(int nthreads)
+{
+    return nthreads < 1 ? 1 : nthreads > MAXT ? MAXT : nthreads;
+}
+
+/* CRC every message of a batch on `nthreads` host threads, messages split
+ * into contiguous byte-balanced slices.  variant: 0 hw 3-way, 1 hw serial,
+ * 2 slicing-by-8, 3 bitwise.  Returns 0. */
+int oracle_crc32c_batch(const uint8_t *arena, const uint64_t *off, const uint32_t *len,
+                        const uint32_t *seed, uint32_t *out, size_t n, int nthreads, int variant)
+{
+    nthreads = clamp_threads(nthreads);
+    pthread_once(&g_tab_once, init_tables);
+    struct batch_job jobs[MAXT];
+    pthread_t th[MAXT];
+    split_jobs(jobs, nthreads, arena, off, len, seed, out, n, variant);
     for (int t = 1; t < nthreads; ++t) {
         pthread_create(&th[t], NULL, batch_worker, &jobs[t]);
     }
@@ -354,18 +363,88 @@ int oracle_crc32c_batch(const uint8_t *arena, const uint64_t *off, const uint32_
     return 0;
 }
 
-/* Wall-clock seconds for `reps` passes of oracle_crc32c_batch (bench helper). */
+/* Timing pool: the worker threads are created once, before the clock
+ * starts, and every pass is bracketed by two barrier waits, so a pass times
+ * the CRCs (and one barrier), not thread start-up. */
+struct pool_arg {
+    struct batch_job *job;
+    pthread_barrier_t *bar;
+    int passes;
+};
+
+static void *pool_worker(void *arg)
+{
+    struct pool_arg *p = (struct pool_arg *)arg;
+    for (int r = 0; r < p->passes; ++r) {
+        pthread_barrier_wait(p->bar);
+        batch_worker(p->job);
+        pthread_barrier_wait(p->bar);
+    }
+    return NULL;
+}
+
+static double now_s(void)
+{
+    struct timespec a;
+    clock_gettime(CLOCK_MONOTONIC, &a);
+    return (double)a.tv_sec + 1e-9 * (double)a.tv_nsec;
+}
+
+/* Wall-clock seconds for `reps` passes over the batch on `nthreads` threads
+ * (bench helper): threads created before the clock starts and one untimed
+ * warm-up pass first. */
 double oracle_time_batch(const uint8_t *arena, const uint64_t *off, const uint32_t *len,
                          const uint32_t *seed, uint32_t *out, size_t n, int nthreads,
                          int variant, int reps)
 {
-    struct timespec a, b;
-    clock_gettime(CLOCK_MONOTONIC, &a);
-    for (int r = 0; r < reps; ++r) {
-        oracle_crc32c_batch(arena, off, len, seed, out, n, nthreads, variant);
+    nthreads = clamp_threads(nthreads);
+    pthread_once(&g_tab_once, init_tables);
+    struct batch_job jobs[MAXT];
+    pthread_t th[MAXT];
+    struct pool_arg args[MAXT];
+    pthread_barrier_t bar;
+    split_jobs(jobs, nthreads, arena, off, len, seed, out, n, variant);
+    pthread_barrier_init(&bar, NULL, (unsigned)nthreads);
+    const int passes = reps + 1;
+    for (int t = 1; t < nthreads; ++t) {
+        args[t].job = &jobs[t];
+        args[t].bar = &bar;
+        args[t].passes = passes;
+        pthread_create(&th[t], NULL, pool_worker, &args[t]);
     }
-    clock_gettime(CLOCK_MONOTONIC, &b);
-    return (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+    double t0 = 0;
+    for (int r = 0; r < passes; ++r) {
+        if (r == 1) {
+            t0 = now_s();  /* after the warm-up pass */
+        }
+        pthread_barrier_wait(&bar);
+        batch_worker(&jobs[0]);
+        pthread_barrier_wait(&bar);
+    }
+    const double dt = now_s() - t0;
+    for (int t = 1; t < nthreads; ++t) {
+        pthread_join(th[t], NULL);
+    }
+    pthread_barrier_destroy(&bar);
+    return dt;
+}
+
+/* The reference's own benchmark loop (bmqp_crc32c.t.cpp:1116-1120): one
+ * buffer CRC'd `iters` times on the calling thread after one untimed call.
+ * Returns wall-clock seconds; *crc_out = the last CRC (keeps the loop live). */
+double oracle_time_repeat(const uint8_t *buf, uint32_t length, int iters, int variant,
+                          uint32_t *crc_out)
+{
+    pthread_once(&g_tab_once, init_tables);
+    crc_fn fn = pick(variant);
+    uint32_t c = fn(buf, length, 0u);
+    const double t0 = now_s();
+    for (int l = 0; l < iters; ++l) {
+        c ^= fn(buf, length, 0u);
+    }
+    const double dt = now_s() - t0;
+    *crc_out = c;
+    return dt;
 }
 
 /* Deterministic synthetic payload bytes shared with the device generator:

@@ -25,6 +25,12 @@ Sources (all in /root/reference, read as text):
       UPDATE and one COMMIT strictly between offsets 88 and 388).
   * queueop_result.txt / summary_queueop_journalop_result.txt: the journal's
       QueueOp CREATION at offset 104 for that key, and its record counts.
+  * journalop_result.txt: every JOURNAL_OP sync point of the journal (index,
+      offset, PSN, epoch, sync point type, SyncPt PSN, node, DATA offset).
+  * summary_result_with_queue_info.txt: per-queue record counts (queue
+      26DACDC974: 2 message, 1 confirm, 1 delete, 4 records), message counts
+      and the journal's last sync point (offset 764, PSN 2/4, DATA 11 dwords,
+      QLIST 32 words).
   * RFC 3720 section B.4 (iSCSI CRC32C test patterns) as external known answers.
 """
 import json
@@ -147,6 +153,8 @@ def main():
     }
     out["csl"] = csl_fixture()
     out["journal_queue_ops"] = queue_op_fixture()
+    out["journal_ops"] = journal_op_fixture()
+    out["queue_summary"] = queue_summary_fixture()
     assert out["csl"]["queue_key"] == out["journal_queue_ops"]["creation"]["queue_key"]
     with open(os.path.join(HERE, "crc32c_vectors.json"), "w") as f:
         json.dump(out, f, indent=1)
@@ -226,6 +234,78 @@ def queue_op_fixture():
         "journal_op_records": count("Number of journalOp records"),
     }
     assert out["creation"]["offset"] == 104 and out["creation"]["op"] == "CREATION", out
+    return out
+
+
+SYNC_POINT_TYPES = {"REGULAR": 1, "ROLLOVER": 2}  # SyncPointType (mqbs_filestoreprotocol.h:1901)
+
+
+def journal_op_fixture():
+    """journalop_result.txt: the JOURNAL_OP records bmqstoragetool lists."""
+    txt = open(os.path.join(DATA_DIR, "journalop_result.txt")).read()
+    recs = []
+    for blk in txt.split("RecordType      : ")[1:]:
+        def field(name):
+            return re.search(r"\b" + name + r"\s*:\s*(\S+)", blk).group(1)
+        assert blk.startswith("JOURNAL_OP") and field("JournalOpType") == "SYNCPOINT", blk
+        recs.append({"index": int(field("Index")), "offset": int(field("Offset")),
+                     "primary_lease_id": int(field("PrimaryLeaseId")),
+                     "sequence_number": int(field("SequenceNumber")),
+                     "epoch": int(field("Epoch")),
+                     "sync_point_type": SYNC_POINT_TYPES[field("SyncPointType")],
+                     "sync_pt_primary_lease_id": int(field("SyncPtPrimaryLeaseId")),
+                     "sync_pt_sequence_number": int(field("SyncPtSequenceNumber")),
+                     "primary_node_id": int(field("PrimaryNodeId")),
+                     "data_file_offset_dwords": int(field("DataFileOffsetDwords"))})
+    n = int(re.search(r"(\d+) journalOp record\(s\) found", txt).group(1))
+    assert n == len(recs) == 8 and recs[0]["offset"] == 44 and recs[-1]["offset"] == 764, recs
+    return {"records": recs, "count": n}
+
+
+def queue_summary_fixture():
+    """summary_result_with_queue_info.txt: message and per-queue record counts
+    and the journal's last sync point."""
+    txt = open(os.path.join(DATA_DIR, "summary_result_with_queue_info.txt")).read()
+
+    def num(label):
+        return int(re.search(label + r"\s*:\s*(\d+)", txt).group(1))
+    q = txt[txt.index("Number of records per Queue:"):txt.index("Details of journal file:")]
+    queues = []
+    for blk in q.split("Queue Key             : ")[1:]:
+        def qf(label):
+            return int(re.search(label + r"\s*:\s*(\d+)", blk).group(1))
+        queues.append({"queue_key": blk.split()[0],
+                       "uri": re.search(r"Queue URI\s*:\s*(\S+)", blk).group(1),
+                       "total_records": qf("Total Records"),
+                       "queue_op_records": qf("Num Queue Op Records"),
+                       "message_records": qf("Num Message Records"),
+                       "confirm_records": qf("Num Confirm Records"),
+                       "delete_records": qf("Num Delete Records")})
+    sp = txt[txt.index("Journal SyncPoint"):]
+    out = {
+        "total_messages": num("Total number of messages"),
+        "partially_confirmed": num("Number of partially confirmed messages"),
+        "confirmed": num("Number of confirmed messages"),
+        "outstanding": num("Number of outstanding messages"),
+        "total_records": num("Total number of records"),
+        "queues": queues,
+        "last_sync_point": {
+            "last_valid_record_offset": int(re.search(r"Last Valid Record Offset\s*:\s*(\d+)",
+                                                      sp).group(1)),
+            "offset": int(re.search(r"Last Valid SyncPoint Offset\s*:\s*(\d+)", sp).group(1)),
+            "epoch": int(re.search(r"SyncPoint Epoch\s*:\s*(\d+)", sp).group(1)),
+            "sequence_number": int(re.search(r"SyncPoint SeqNum\s*:\s*(\d+)", sp).group(1)),
+            "primary_node_id": int(re.search(r"SyncPoint Primary NodeId\s*:\s*(\d+)",
+                                             sp).group(1)),
+            "primary_lease_id": int(re.search(r"SyncPoint Primary LeaseId\s*:\s*(\d+)",
+                                              sp).group(1)),
+            "data_file_offset_dwords": int(re.search(
+                r"SyncPoint DataFileOffset \(DWORDS\)\s*:\s*(\d+)", sp).group(1)),
+            "qlist_file_offset_words": int(re.search(
+                r"SyncPoint QlistFileOffset \(WORDS\)\s*:\s*(\d+)", sp).group(1)),
+        },
+    }
+    assert len(queues) == 1 and queues[0]["total_records"] == 4, queues
     return out
 
 

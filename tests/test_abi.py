@@ -53,13 +53,13 @@ def test_library_contains_gfx950_code_object():
 def test_version_and_error_string():
     lib = ctypes.CDLL(LIB)
     lib.bmqcrc_version.restype = ctypes.c_uint32
-    assert lib.bmqcrc_version() >> 16 == 2
+    assert lib.bmqcrc_version() >> 16 == 2 and lib.bmqcrc_version() & 0xffff >= 5
     lib.bmqcrc_last_error.restype = ctypes.c_char_p
     assert isinstance(lib.bmqcrc_last_error(), bytes)
 
 
 def test_opts_layout_matches_the_header(tmp_path):
-    # bmqcrc_opts as the C compiler lays it out (ABI 2.4 appends max_len) and
+    # bmqcrc_opts as the C compiler lays it out (ABI 2.4 appends max_len, 2.5 min_len) and
     # as the ctypes binding does: same size, same field offsets
     from blazingmq_amd import _native as N
     src = tmp_path / "opts.c"

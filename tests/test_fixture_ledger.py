@@ -9,6 +9,13 @@ test_gpu_extensions.py).
   (queue key 26DACDC974) and test_cslfile.py's searches.
 * queueop_result.txt / summary_queueop_journalop_result.txt -- the journal's
   QueueOp CREATION at 104 and its record counts.
+* journalop_result.txt -- the journal's eight SYNCPOINT records (offset, PSN,
+  epoch, sync point type and PSN, node, DATA offset); with them the recovery
+  walk's sync point checks (mqbs_filestore.cpp:1647-1713) are pinned to the
+  reference's own file: mutating one sync point's PSN gives the reference's
+  rc at that record, in the native walk and in the Python restatement.
+* summary_result_with_queue_info.txt -- per-queue record counts, message
+  counts and the journal's last sync point.
 
 All extracted into tests/golden/crc32c_vectors.json by make_golden.py.  The
 native ledger walk (bmqcrc_csl_scan) must find these records, and every CRC
@@ -19,6 +26,7 @@ padding).  CSL-mode recovery of the journal fixture with the ledger's key
 import os
 
 import numpy as np
+import pytest
 
 import oracle
 from blazingmq_amd import csl
@@ -137,3 +145,111 @@ def test_csl_mode_recovery_with_the_ledgers_queue_key(golden):
         r = fn(j, d, with_csl=True, queue_keys=[b"\x26\xda\xcd\xc9\x75"])
         assert (r["recovery_rc"], r["error_record_offset"]) == \
             (S.RC_INVALID_QUEUE_KEY, golden["journal_queue_ops"]["creation"]["offset"])
+
+
+def _be(r, off, n):
+    return int.from_bytes(r[off:off + n], "big")
+
+
+def _record_offsets(j):
+    _, last = S.journal_bounds(j)
+    fh = S.parse_file_header(j, S.FILE_TYPE_JOURNAL)
+    start = fh + int(j[fh]) * S.WORD
+    return start, list(range(start, last + 1, S.JOURNAL_RECORD_SIZE))
+
+
+def test_journal_sync_points_match_bmqstoragetool(golden):
+    """journalop_result.txt, field by field from the file (JournalOpRecord,
+    mqbs_filestoreprotocol.h:1953: sync point type @23, JournalOpType @24,
+    SyncPt sequence @28/@32, node @36, SyncPt lease @40, DATA offset dwords
+    @44), and summary_result_with_queue_info.txt's last sync point (the
+    native journal bounds and the Python restatement agree with it)."""
+    j, _ = _journal()
+    g = golden["journal_ops"]
+    start, offs = _record_offsets(j)
+    jops = [o for o in offs if int(j[o]) >> 4 == S.REC_JOURNAL_OP]
+    assert jops == [r["offset"] for r in g["records"]] and len(jops) == g["count"] == 8
+    for want in g["records"]:
+        r = j[want["offset"]:want["offset"] + S.JOURNAL_RECORD_SIZE].tobytes()
+        assert (want["offset"] - start) // S.JOURNAL_RECORD_SIZE == want["index"]
+        assert _be(r, 8, 4) == want["primary_lease_id"]
+        assert (_be(r, 2, 2) << 32 | _be(r, 4, 4)) == want["sequence_number"]
+        assert _be(r, 12, 8) == want["epoch"]
+        assert r[23] == want["sync_point_type"] and _be(r, 24, 4) == S.JOURNAL_OP_SYNCPOINT
+        assert (_be(r, 28, 4) << 32 | _be(r, 32, 4)) == want["sync_pt_sequence_number"]
+        assert _be(r, 36, 4) == want["primary_node_id"]
+        assert _be(r, 40, 4) == want["sync_pt_primary_lease_id"]
+        assert _be(r, 44, 4) == want["data_file_offset_dwords"]
+    ls = golden["queue_summary"]["last_sync_point"]
+    assert S.journal_bounds(j) == S.journal_bounds_py(j) == (ls["offset"],
+                                                           ls["last_valid_record_offset"])
+    r = j[ls["offset"]:ls["offset"] + S.JOURNAL_RECORD_SIZE].tobytes()
+    assert (_be(r, 28, 4) << 32 | _be(r, 32, 4)) == ls["sequence_number"]
+    assert (_be(r, 40, 4), _be(r, 36, 4), _be(r, 12, 8)) == (ls["primary_lease_id"],
+                                                            ls["primary_node_id"], ls["epoch"])
+    assert (_be(r, 44, 4), _be(r, 48, 4)) == (ls["data_file_offset_dwords"],
+                                              ls["qlist_file_offset_words"])
+
+
+def _mutate(j, off, field_off, value, n=4):
+    m = j.copy()
+    m[off + field_off:off + field_off + n] = np.frombuffer(value.to_bytes(n, "big"), np.uint8)
+    return m
+
+
+@pytest.mark.parametrize("at", [764, 704, 584, 524, 164])
+def test_sync_point_mutations_give_the_references_codes(golden, at):
+    """The recovery walk's sync point checks in the reference's order
+    (mqbs_filestore.cpp:1647-1713) on the reference's journal: a sync point
+    whose SyncPt sequence number disagrees with the PSN chain fails with
+    rc_INVALID_SEQ_NUMBER at that record, one whose SyncPt lease id is ahead
+    of its record's (or zero) with rc_INVALID_PRIMARY_LEASE_ID, a zero SyncPt
+    sequence with rc_INVALID_SEQ_NUMBER, a DATA offset past the DATA file with
+    rc_INVALID_DATA_OFFSET (:1589-1606).  Native walk and Python restatement
+    alike; the unmodified journal recovers with rc 0."""
+    j, d = _journal()
+    want = {r["offset"]: r for r in golden["journal_ops"]["records"]}[at]
+    sp_seq, sp_lease = want["sync_pt_sequence_number"], want["sync_pt_primary_lease_id"]
+    cases = [
+        (_mutate(j, at, 32, (sp_seq + 1) & 0xFFFFFFFF), S.RC_INVALID_SEQ_NUMBER),
+        (_mutate(_mutate(j, at, 28, 0), at, 32, 0), S.RC_INVALID_SEQ_NUMBER),
+        (_mutate(j, at, 40, sp_lease + 1), S.RC_INVALID_PRIMARY_LEASE_ID),
+        (_mutate(j, at, 40, 0), S.RC_INVALID_PRIMARY_LEASE_ID),
+        (_mutate(j, at, 44, d.size // S.DWORD + 1), S.RC_INVALID_DATA_OFFSET),
+    ]
+    for fn in (S.scan_partition, S.recovery_selection_py):
+        assert fn(j, d)["recovery_rc"] == 0
+        for m, rc in cases:
+            r = fn(m, d)
+            assert (r["recovery_rc"], r["error_record_offset"]) == (rc, at), (fn, rc)
+
+
+def test_queue_record_counts_match_bmqstoragetool(golden):
+    """summary_result_with_queue_info.txt: queue 26DACDC974 has 4 records --
+    2 MESSAGE, 1 CONFIRM, 1 DELETION (bmqstoragetool's summary leaves the
+    queue's QueueOp CREATION out unless asked; summary_queueop_journalop
+    counts it) -- of 2 messages 1 is confirmed and 1 outstanding, and that
+    one is what recovery CRCs."""
+    j, d = _journal()
+    q = golden["queue_summary"]
+    queue = q["queues"][0]
+    key = bytes.fromhex(queue["queue_key"])
+    assert queue["queue_key"] == golden["csl"]["queue_key"]
+    _, offs = _record_offsets(j)
+    key_at = {S.REC_MESSAGE: 22, S.REC_CONFIRM: 22, S.REC_DELETION: 23, S.REC_QUEUE_OP: 22}
+    counts = {t: 0 for t in key_at}
+    for o in offs:
+        t = int(j[o]) >> 4
+        if t in key_at and j[o + key_at[t]:o + key_at[t] + 5].tobytes() == key:
+            counts[t] += 1
+    assert counts[S.REC_MESSAGE] == queue["message_records"] == q["total_messages"] == 2
+    assert counts[S.REC_CONFIRM] == queue["confirm_records"] == 1
+    assert counts[S.REC_DELETION] == queue["delete_records"] == 1
+    assert counts[S.REC_MESSAGE] + counts[S.REC_CONFIRM] + counts[S.REC_DELETION] == \
+        queue["total_records"] == q["total_records"] == 4
+    assert counts[S.REC_QUEUE_OP] == golden["journal_queue_ops"]["creation_ops"] == 1
+    assert queue["queue_op_records"] == 0
+    for fn in (S.scan_partition, S.recovery_selection_py):
+        r = fn(j, d)
+        assert len(r["record_offset"]) == q["outstanding"] == 1
+        assert q["total_messages"] - q["outstanding"] == q["confirmed"] == 1

@@ -407,55 +407,72 @@ def test_shape_hint_misprediction(cuda):
 
 
 def test_planner_map_given_up(cuda):
-    # Round 3: ragged batches are planned by one kernel whose blocks meet once,
+    # Ragged batches are planned by one kernel whose blocks meet once,
     # grid-wide.  When they cannot all run at once a block stops waiting after
-    # bmqcrc_plan_wait's limit and the map is given up: the fold then searches
-    # seg_first.  With the limit at 0 every map is given up; the CRCs must not
-    # change, and the counter must say so.  The default limit maps normally.
+    # bmqcrc_plan_wait's limit and the map is given up; every block still
+    # writes seg_first and the out[] initialisation, and the fold then maps
+    # segments by searching seg_first (round 4; round 3 folded every message
+    # whole in one lane, so a multi-MiB message held its wave for its whole
+    # length).  A zero limit gives every map up before the first poll: the
+    # CRCs must not change, the counter must count every such batch, and a
+    # given-up batch holding 32 MiB messages must stay within a small factor
+    # of the mapped step.  The default limit maps normally.
+    import time
+
     import torch
     from blazingmq_amd import last_launch, plan_wait
     rng = np.random.default_rng(91)
-    arena_np = rng.integers(0, 256, size=64 << 20, dtype=np.uint8)
+    arena_np = rng.integers(0, 256, size=96 << 20, dtype=np.uint8)
     arena = torch.from_numpy(arena_np).to(cuda)
     s = torch.cuda.Stream(cuda)
     # more than four planner tiles per block (> 1.3M messages): the
     # single-pass planner, not the round-2 pair
     lens = np.concatenate([rng.integers(0, 200, size=1_400_000),
                            rng.integers(0, 300000, size=300),
-                           rng.integers(1000, 9000, size=5000)]).astype(np.uint32)
+                           rng.integers(1000, 9000, size=5000),
+                           np.full(3, 32 << 20)]).astype(np.uint32)
     rng.shuffle(lens)
     offs = (rng.random(lens.size) * (arena_np.size - lens + 1)).astype(np.int64)
     seeds = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64).astype(np.uint32)
     exp = oracle.batch(arena_np, offs, lens, seeds, nthreads=8)
+    d_offs = torch.from_numpy(offs).to(cuda)
+    d_lens = torch.from_numpy(lens.view(np.int32)).to(cuda)
+    d_seeds = torch.from_numpy(seeds.view(np.int32)).to(cuda)
 
-    def run():
-        got = Crc32c.calculate_batch(arena, torch.from_numpy(offs).to(cuda),
-                                     torch.from_numpy(lens.view(np.int32)).to(cuda),
-                                     torch.from_numpy(seeds.view(np.int32)).to(cuda),
-                                     stream=s, seg_bytes=2048)
+    def run(reps=1):
+        torch.cuda.synchronize(cuda)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            got = Crc32c.calculate_batch(arena, d_offs, d_lens, d_seeds, stream=s,
+                                         seg_bytes=2048, sync=False)
         s.synchronize()
+        dt = (time.perf_counter() - t0) / reps
         bad = np.nonzero(got.cpu().numpy().view(np.uint32) != exp)[0]
         assert bad.size == 0, [(int(i), int(lens[i])) for i in bad[:8]]
+        return dt
 
     v0 = plan_wait(cuda.index, s)
-    for _ in range(3):
-        run()
+    run()
+    t_map = run(5)
     assert last_launch(cuda.index, s)["kernels"] == 2  # k_plan_map + k_fold
     assert plan_wait(cuda.index, s, 0) == v0  # a lone stream: every map was kept
-    for _ in range(3):
-        run()
+    run()
+    t_void = run(5)
     v1 = plan_wait(cuda.index, s, 1000)
-    assert v1 > v0
+    assert v1 == v0 + 6  # the zero limit gives up every launch's map
+    print("mapped %.3f ms, given up %.3f ms per batch" % (1e3 * t_map, 1e3 * t_void))
+    assert t_void < 2.0 * t_map + 1e-3, (t_map, t_void)
     run()  # back to mapping
     assert plan_wait(cuda.index, s) == v1
 
 
-def test_planners_on_two_streams_at_once(cuda):
+def test_planners_on_two_streams_at_once(cuda, record_property):
     # Two large ragged batches enqueued on two streams without waiting: their
     # single-pass planners may share the GPU, so a planner's blocks may not
     # all be resident together and a block may give its map up (exact either
-    # way).  Every CRC of both batches must match, with and without a wait
-    # limit that forces the give-up.
+    # way).  Every CRC of both batches must match, with the default wait
+    # limit and with a zero limit that gives every map up; the number of
+    # given-up maps is recorded (test property plan_voided).
     import torch
     from blazingmq_amd import plan_wait
     rng = np.random.default_rng(92)
@@ -471,14 +488,22 @@ def test_planners_on_two_streams_at_once(cuda):
         batches.append((torch.from_numpy(offs).to(cuda), torch.from_numpy(lens.view(np.int32)).to(cuda),
                         oracle.batch(arena_np, offs, lens, None, nthreads=8)))
     torch.cuda.synchronize(cuda)
+    voided = {}
     for wait_us in (1000, 0, 1000):
-        for s in streams:
-            plan_wait(cuda.index, s, wait_us)
-        outs = [Crc32c.calculate_batch(arena, o, ln, None, stream=s, sync=False)
-                for (o, ln, _), s in zip(batches, streams)]
+        before = [plan_wait(cuda.index, s, wait_us) for s in streams]
+        for _ in range(3):
+            outs = [Crc32c.calculate_batch(arena, o, ln, None, stream=s, sync=False)
+                    for (o, ln, _), s in zip(batches, streams)]
         torch.cuda.synchronize(cuda)
         for (_, _, exp), got in zip(batches, outs):
             assert np.array_equal(got.cpu().numpy().view(np.uint32), exp)
+        after = [plan_wait(cuda.index, s, wait_us) for s in streams]
+        n = sum(b - a for a, b in zip(before, after))
+        voided["wait_%dus" % wait_us] = voided.get("wait_%dus" % wait_us, 0) + n
+        if wait_us == 0:
+            assert n == 6  # 3 batches x 2 streams, every map given up
+    record_property("plan_voided", voided)
+    print("plan_voided", voided)
 
 
 def test_max_length_messages(cuda):
