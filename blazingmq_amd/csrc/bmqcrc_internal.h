@@ -74,9 +74,10 @@ struct BatchArgs {
                                //    runs before k_fold; 0: skipped (the previous batch on this
                                //    workspace was closed-form) and a ragged batch maps segments
                                //    by binary search instead -- slower, never wrong
-    uint32_t* shape_hint;      // host-mapped word or nullptr: k_fold writes kHintIdentity,
+    uint32_t* shape_hint;      // host-mapped words or nullptr: k_fold writes [0] kHintIdentity,
                                // kHintClosed or kHintRagged, the host reads it when planning
-                               // the next batch
+                               // the next batch; [1] the epoch of the last launch whose
+                               // k_plan_map gave its map up (sticky)
     // Speculative single launch (spec = u > 0): the previous batch on this
     // workspace had u segments per message (u = 1, or u dividing 64), so no
     // planner runs and k_fold folds segment k of message m in slot m*u + k
@@ -95,7 +96,16 @@ struct BatchArgs {
     uint32_t plan_epoch;       // k_plan_map launch tag on this workspace, never 0
     uint64_t map_wait_ticks;   // k_plan_map's grid-wide wait limit (100 MHz wall clock)
     uint32_t class_desc;       // k_plan_map: size classes in descending order (short schedules)
+    // 1: plan this ragged batch with the meeting-free pair k_plan<true> +
+    // k_plan_sort instead of k_plan_map (the host does so for a while after
+    // a map on this workspace was given up: the GPU is shared, kPairAfterVoid)
+    uint32_t pair;
 };
+
+// Ragged batches planned with the pair after k_fold reports a given-up map
+// on the workspace (shape_hint[1] = that launch's epoch), before the
+// single-pass planner is tried again.
+constexpr uint32_t kPairAfterVoid = 16;
 
 // k_fold groups per wave below which k_plan_map orders the size classes
 // largest first: the schedule's tail is then one-line groups instead of a
@@ -115,7 +125,7 @@ constexpr uint32_t kSegLast = 0x80000000u;  // seginfo: the entry is its message
 // profiles/r03/ab/planner_stamps/).
 inline bool single_pass_planner(const BatchArgs& a)
 {
-    return !(a.tune & 128u);
+    return !(a.tune & 128u) && !a.pair;
 }
 
 constexpr uint32_t kHintUnknown = 0;

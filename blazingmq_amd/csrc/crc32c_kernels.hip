@@ -935,6 +935,10 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
                            : (hint_uni || pt.overflow) ? kHintClosed
                                                   : kHintRagged,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (map_void) {  // the GPU was shared: the host plans with the pair for a while
+            __hip_atomic_store(a.shape_hint + 1, a.plan_epoch, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 
     const uint32_t rd_off = (uint32_t)lane * 128u + (((uint32_t)lane >> 1) & 7u) * 16u;

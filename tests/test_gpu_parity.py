@@ -466,6 +466,38 @@ def test_planner_map_given_up(cuda):
     assert plan_wait(cuda.index, s) == v1
 
 
+def test_given_up_map_switches_the_workspace_to_the_pair(cuda):
+    # After k_fold reports a given-up map on a workspace, the host plans that
+    # workspace's next kPairAfterVoid (16) ragged batches with the meeting-free
+    # pair k_plan + k_plan_sort (3 kernels), then tries the single-pass
+    # planner again (2 kernels).  A zero limit (the test hook) never switches.
+    import torch
+    from blazingmq_amd import last_launch, plan_wait
+    rng = np.random.default_rng(93)
+    arena_np = rng.integers(0, 256, size=16 << 20, dtype=np.uint8)
+    arena = torch.from_numpy(arena_np).to(cuda)
+    s = torch.cuda.Stream(cuda)
+    lens = np.concatenate([rng.integers(0, 300, size=1_400_000),
+                           rng.integers(0, 100000, size=100)]).astype(np.uint32)
+    rng.shuffle(lens)
+    offs = (rng.random(lens.size) * (arena_np.size - lens + 1)).astype(np.int64)
+    exp = oracle.batch(arena_np, offs, lens, None, nthreads=8)
+    d_offs = torch.from_numpy(offs).to(cuda)
+    d_lens = torch.from_numpy(lens.view(np.int32)).to(cuda)
+
+    def run():
+        got = Crc32c.calculate_batch(arena, d_offs, d_lens, stream=s, seg_bytes=2048)
+        assert np.array_equal(got.cpu().numpy().view(np.uint32), exp)
+        return last_launch(cuda.index, s)["kernels"]
+
+    plan_wait(cuda.index, s, 0)
+    assert [run() for _ in range(3)] == [2, 2, 2]  # the hook: every map given up, no switch
+    v = plan_wait(cuda.index, s, 1000)
+    kernels = [run() for _ in range(18)]
+    assert kernels == [3] * 16 + [2, 2], kernels
+    assert plan_wait(cuda.index, s) == v  # the pair and the retried single pass kept their maps
+
+
 def test_planners_on_two_streams_at_once(cuda, record_property):
     # Two large ragged batches enqueued on two streams without waiting: their
     # single-pass planners may share the GPU, so a planner's blocks may not

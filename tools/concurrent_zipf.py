@@ -36,7 +36,9 @@ def main():
     p.add_argument("--streams", default="2,4")
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--wait-us", type=int, default=1000)
+    p.add_argument("--seg-bytes", type=int, default=0, help="0: automatic")
+    p.add_argument("--wait-us", default="1000",
+                   help="bmqcrc_plan_wait limits to run the concurrent legs with (comma list)")
     a = p.parse_args()
     dev = torch.device("cuda", 0)
     _, gen, seed, _ = bench.CONFIGS["zipf_4M"]
@@ -55,11 +57,18 @@ def main():
         outs = [torch.empty(hi - lo, dtype=torch.int32, device=dev) for lo, hi in parts]
         for s in streams:
             bmq.plan_wait(0, s, wait_us)
+        # each part is its own arena (a partition's DATA file): its bytes and
+        # offsets relative to them, so the automatic shape sees the part's size
+        views = []
+        for lo, hi in parts:
+            base = int(offs_np[lo]) if hi > lo else 0
+            nb = int(offs_np[hi - 1]) + int(lens_np[hi - 1]) - base if hi > lo else 0
+            views.append((arena[base:base + nb], offs[lo:hi] - base, lens[lo:hi]))
 
         def step():
-            for (lo, hi), s, o in zip(parts, streams, outs):
-                Crc32c.calculate_batch(arena, offs[lo:hi], lens[lo:hi], None, o, stream=s,
-                                       sync=False)
+            for (ar, of, ln), s, o in zip(views, streams, outs):
+                Crc32c.calculate_batch(ar, of, ln, None, o, stream=s, sync=False,
+                                       seg_bytes=a.seg_bytes)
         for _ in range(a.warmup):
             step()
         torch.cuda.synchronize(dev)
@@ -74,7 +83,8 @@ def main():
         return dt, v1 - v0, got
 
     one = torch.cuda.Stream(dev)
-    t_map, v_map, ref = leg("whole", [(0, n)], [one], a.wait_us)
+    waits = [int(x) for x in a.wait_us.split(",") if x]
+    t_map, v_map, ref = leg("whole", [(0, n)], [one], waits[0])
     # the reference result: oracle-checked on a sample
     import oracle
     rng = np.random.default_rng(7)
@@ -86,7 +96,7 @@ def main():
     def emit(leg_name, dt, voided, got, **kw):
         print(json.dumps(dict({
             "leg": leg_name, "ms_per_step": round(1e3 * dt, 4), "GiBps": round(gib / dt, 1),
-            "plan_voided": voided, "steps": a.steps,
+            "plan_voided": voided, "steps": a.steps, "seg_bytes": a.seg_bytes or "auto",
             "equal_to_whole_mapped": bool(np.array_equal(got, ref))}, **kw)), flush=True)
 
     emit("whole_one_stream_mapped", t_map, v_map, ref, oracle_sample_mismatches=bad,
@@ -97,12 +107,13 @@ def main():
     for S in [int(x) for x in a.streams.split(",") if x]:
         parts = [rank_slice(lens_np, r, S) for r in range(S)]
         streams = [torch.cuda.Stream(dev) for _ in range(S)]
-        dt, v, got = leg("conc%d" % S, parts, streams, a.wait_us)
-        emit("%d_parts_%d_streams_at_once" % (S, S), dt, v, got, planner_launches=S * a.steps,
-             ratio_to_mapped=round(dt / t_map, 3))
-        dt, v, got = leg("serial%d" % S, parts, [one] * S, a.wait_us)
+        for w in waits:
+            dt, v, got = leg("conc%d" % S, parts, streams, w)
+            emit("%d_parts_%d_streams_at_once" % (S, S), dt, v, got, planner_launches=S * a.steps,
+                 ratio_to_mapped=round(dt / t_map, 3), plan_wait_us=w)
+        dt, v, got = leg("serial%d" % S, parts, [one] * S, waits[0])
         emit("%d_parts_one_stream" % S, dt, v, got, planner_launches=S * a.steps,
-             ratio_to_mapped=round(dt / t_map, 3))
+             ratio_to_mapped=round(dt / t_map, 3), plan_wait_us=waits[0])
     return 0
 
 
