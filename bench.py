@@ -600,7 +600,7 @@ def main():
     planned_launch = bmq.last_launch(local, stream)
     voided2 = bmq.plan_wait(local, stream, wait_us)
     # ... and with the prediction dropped before every step but the batch's
-    # length bounds declared (bmqcrc_opts.max_len / min_len, ABI 2.4): what a
+    # length bounds declared (bmqcrc_opts.max_len / min_len, ABI 2.4 / 2.5): what a
     # caller that knows its message sizes pays when shapes alternate.
     max_len = int(lens_np.max()) if n else 0
     min_len = int(lens_np.min()) if n else 0
@@ -696,6 +696,12 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "k_fold", "kernel_avg_us": round(avg_kern_s * 1e6, 2),
+                         "kernel_time_source": "HIP events around each k_fold launch on its "
+                                               "stream, K extra steps (event-priced: includes "
+                                               "the launch gap, so frac is a lower bound; the "
+                                               "traced kernel time is in profiles/)",
+                         "frac_per_step": round(alg_bytes / (elapsed / args.steps) / 1e9
+                                                / HBM_PEAK_GBS, 4),
                          "alg_bytes_per_launch": alg_bytes},
             "parity": {"checked_msgs": checked, "mismatches": bad},
             "kernels_per_step": launch["kernels"],

@@ -27,7 +27,9 @@ constexpr int kBuckets = 16;            // segment size classes: floor(log2(line
 // forces 2, bit4 always builds the size-class map (no shape prediction),
 // bit5 reads one- and two-line groups non-temporally too, bit7 plans ragged
 // batches with the round-2 pair k_plan<true> + k_plan_sort instead of the
-// single-pass k_plan_map, bit9 gives planner blocks whole tiles (A/B).
+// single-pass k_plan_map, bit9 gives planner blocks whole tiles, bit10 keeps
+// two 4-wave k_fold blocks per CU with static group shares (round 3's schedule)
+// instead of one 8-wave block claiming groups dynamically (A/B).
 #ifndef BMQCRC_TUNE_BITS
 #define BMQCRC_TUNE_BITS 0u
 #endif

@@ -817,39 +817,78 @@ __device__ __forceinline__ SegDesc fetch_desc(const BatchArgs& a, SegRef r, bool
     return d;
 }
 
+#ifndef BMQCRC_FOLD_DIAG
+#define BMQCRC_FOLD_DIAG 0  // 1: per-wave wall-clock stamps of the last k_fold launch
+                            // (timing diagnostics, tools/fold_trace_diag.py); product: 0
+#endif
+#if BMQCRC_FOLD_DIAG
+// diagnostic build only: per wave (entry, prologue done, first loads issued,
+// first group folded, last group's lines folded, loop done, end), read by
+// bmqcrc_diag_fold_trace
+constexpr int kFoldTraceWaves = 4096;
+__device__ unsigned long long g_fold_trace[kFoldTraceWaves][8];
+#define FOLD_STAMP(k)                                                              \
+    if (lane == 0 && g0 < (uint32_t)kFoldTraceWaves) {                             \
+        g_fold_trace[g0][k] = wall_clock64();                                      \
+    }
+#else
+#define FOLD_STAMP(k)
+#endif
+
+// Groups whose speculative first pass skipped a message (a block's list for
+// the second pass; past this many the second pass scans the block's groups).
+constexpr uint32_t kLongListCap = 64;
+
 // ONE: a speculative launch predicting one segment per message (spec == 1),
 // compiled apart so the first pass knows k = 0 and nseg = 1 (no planner words,
 // no move to the message end, no run combine).
-template <bool NT, bool ONE>
-__global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
+// WPB: waves per block.  8 = one block of two waves per SIMD per CU (round
+// 4), whose waves take the block's groups from an LDS counter as they go:
+// with two 4-wave blocks per CU and a static grid-stride share each, the
+// CU's second block ran its waves 9 % longer (later start, then less issue
+// share) and the launch ended on it (tools/fold_trace_diag.py,
+// profiles/r04/fold_trace/).  4 = one wave per SIMD (large-message batches,
+// one block per CU) or small batches spread over more CUs.
+template <bool NT, bool ONE, int WPB>
+__global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a)
 {
+    constexpr uint32_t kThreads = WPB * 64;
+    constexpr int kLds = WPB * kSlots * kSlotBytes;
     // remainder tables, DMA slots, move factors (not needed by ONE: no moves
     // in its first pass)
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kTabBytes + kLdsBytes + (ONE ? 0 : kXbBytes)];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kTabBytes + kLds + (ONE ? 0 : kXbBytes)];
+    // group claims: the block owns groups blockIdx.x + k gridDim.x, k = 0, 1,
+    // ...; wave w starts with k = w, later k come from this counter
+    __shared__ uint32_t claim_ctr, long_n;
+    __shared__ uint32_t long_list[kLongListCap];
 
     const int lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t tab_lds = (uint32_t)(uintptr_t)(lds_u8*)lds;
     const uint32_t wave_lds = tab_lds + kTabBytes + wave * (kSlots * kSlotBytes);
-    const uint32_t xb_lds = tab_lds + kTabBytes + kLdsBytes;
+    const uint32_t xb_lds = tab_lds + kTabBytes + kLds;
+    if (threadIdx.x == 0) {
+        claim_ctr = WPB;
+        long_n = 0;
+    }
 
     // Prologue: every load that depends on nothing is issued before the first
     // wait -- the remainder tables, k_plan's block words and the first group's
     // descriptors as if segment = message (true for BMQCRC_F_WHOLE_MESSAGES
     // and for identity batches; discarded otherwise).
-    static_assert(8 * 256 == 8 * kWavesPerBlock * 64, "table fill: 8 words per thread");
-    uint32_t tw[8];
+    constexpr int kTw = 2048 / kThreads, kXw = 1024 / kThreads;  // table words per thread
+    static_assert(kTw * kThreads == 2048 && kXw * kThreads == 1024, "table fill");
+    uint32_t tw[kTw];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const uint32_t t = threadIdx.x + (uint32_t)i * (kWavesPerBlock * 64);
+    for (int i = 0; i < kTw; ++i) {
+        const uint32_t t = threadIdx.x + (uint32_t)i * kThreads;
         tw[i] = c_ty[t >> 8][t & 255u];
     }
-    static_assert(4 * 256 == 4 * kWavesPerBlock * 64, "move factors: 4 words per thread");
-    uint32_t xw[4];
+    uint32_t xw[kXw];
     if (!ONE) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t t = threadIdx.x + (uint32_t)i * (kWavesPerBlock * 64);
+        for (int i = 0; i < kXw; ++i) {
+            const uint32_t t = threadIdx.x + (uint32_t)i * kThreads;
             xw[i] = c_xbytes[t >> 8][t & 255u];
         }
     }
@@ -870,14 +909,24 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     // memory it would be a vector load with a full memory latency per group
     __shared__ uint32_t xneg8[136];
     const uint32_t xn = threadIdx.x < 136u ? c_xneg8[threadIdx.x] : 0u;
-    const uint32_t g0 = blockIdx.x * kWavesPerBlock + wave;
-    const uint32_t sid = g0 * 64u + (uint32_t)lane;
+    [[maybe_unused]] const uint32_t g0 = blockIdx.x * WPB + wave;  // this wave's index in the grid
+    FOLD_STAMP(0)
+#ifdef BMQCRC_LATE_PRIO
+    // A/B: the second half of the grid (the second block of each CU) at a
+    // raised issue priority
+    if (blockIdx.x >= gridDim.x / 2) {
+        __builtin_amdgcn_s_setprio(BMQCRC_LATE_PRIO);
+    }
+#endif
+    // the wave's first group (claim k = wave), as if segment = message
+    const uint32_t gfirst = blockIdx.x + wave * gridDim.x;
+    const uint32_t sid = gfirst * 64u + (uint32_t)lane;
     const SegDesc spec = fetch_desc(a, SegRef{sid, 0u}, sid < a.n);
     // remainder-reduction tables -> LDS (8 KiB, once per block; no DMA in
     // flight yet; plan_reduce's barriers order them before any lookup)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const uint32_t t = threadIdx.x + (uint32_t)i * (kWavesPerBlock * 64);
+    for (int i = 0; i < kTw; ++i) {
+        const uint32_t t = threadIdx.x + (uint32_t)i * kThreads;
         *(lds_u32*)(uintptr_t)(tab_lds + 4u * t) = tw[i];
     }
     if (threadIdx.x < 136u) {
@@ -885,8 +934,8 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     }
     if (!ONE) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t t = threadIdx.x + (uint32_t)i * (kWavesPerBlock * 64);
+        for (int i = 0; i < kXw; ++i) {
+            const uint32_t t = threadIdx.x + (uint32_t)i * kThreads;
             *(lds_u32*)(uintptr_t)(xb_lds + 4u * t) = xw[i];
         }
     }
@@ -941,10 +990,19 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         }
     }
 
+    FOLD_STAMP(1)
     const uint32_t rd_off = (uint32_t)lane * 128u + (((uint32_t)lane >> 1) & 7u) * 16u;
     const uint64_t zero = (uint64_t)(uintptr_t)g_zero_line + 16u * ((uint32_t)lane & 7u);
 
-    const uint32_t stride = gridDim.x * kWavesPerBlock;
+    // claim k of this block = group blockIdx.x + k gridDim.x (>= ngroups: none)
+    const uint32_t nbk = gridDim.x;
+    auto claim = [&]() {
+        uint32_t k = 0;
+        if (lane == 0) {
+            k = atomicAdd(&claim_ctr, 1u);
+        }
+        return blockIdx.x + (uint32_t)__builtin_amdgcn_readfirstlane((int)k) * nbk;
+    };
     const uint32_t seg_shift = (SEG & (SEG - 1u)) == 0 ? (uint32_t)__builtin_ctz(SEG) : 0u;
 
     // One group = 64 segments, one per lane.  Its per-lane geometry and the
@@ -1022,7 +1080,6 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     auto segments = [&](uint32_t len) {
         return len ? (seg_shift ? ((len - 1u) >> seg_shift) : (len - 1u) / SEG) + 1u : 0u;
     };
-    bool long_seen = false;  // speculative: a message of this wave needs the second pass
     // The segment of group gg in this lane (planned or speculative mapping).
     auto setup = [&](const SegDesc& d, uint32_t gg, Group& G) {
         const uint32_t seg = gg * 64u + (uint32_t)lane;
@@ -1033,7 +1090,12 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
             // the wave's second pass (below); with u = 1 an empty message is
             // folded whole (its seed)
             const bool ok = spec_u == 1u ? nseg <= 1u : nseg == spec_u;
-            long_seen |= __ballot(valid && !ok) != 0;
+            if (__ballot(valid && !ok) != 0 && lane == 0) {  // group gg goes on the block's list
+                const uint32_t at = atomicAdd(&long_n, 1u);
+                if (at < kLongListCap) {
+                    long_list[at] = gg;
+                }
+            }
             valid = valid && ok;
             nseg = spec_u;
         }
@@ -1205,16 +1267,23 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
         }
     };
 
-    // Speculative launches only: the wave's messages longer than one segment,
-    // skipped by its first pass, folded with all 64 lanes (lane l: segment
-    // 64c + l of chunk c), one message at a time; the chunks' contributions
-    // are XOR-accumulated in registers and stored once.  A wave never waits
-    // on another, and in the predicted case (every message one segment) no
-    // wave runs this pass.
-    auto second_pass = [&]() {
+    // Speculative launches only: the block's messages of another segment
+    // count than predicted, skipped by the first pass, folded with all 64
+    // lanes of a wave (lane l: segment 64c + l of chunk c), one message at a
+    // time; the chunks' contributions are XOR-accumulated in registers and
+    // stored once.  The groups holding them are on the block's list (all the
+    // block's groups are scanned if it overflowed), shared out over its
+    // waves.  No wave waits on another block, and in the predicted case
+    // (every message as predicted) no wave runs this pass.
+    auto second_pass = [&](uint32_t nlong) {
         bool any = false;
         const uint32_t mpg = 64u / spec_u;  // messages per group
-        for (uint32_t gg = g0; gg < ngroups; gg += stride) {
+        const bool listed = nlong <= kLongListCap;
+        for (uint32_t j = wave;; j += WPB) {
+            const uint32_t gg = listed ? (j < nlong ? long_list[j] : ngroups) : blockIdx.x + j * nbk;
+            if (gg >= ngroups) {
+                break;
+            }
             const uint64_t i = (uint64_t)gg * mpg + (uint32_t)lane;
             const bool mine = (uint32_t)lane < mpg && i < a.n;
             const uint32_t len = mine ? a.lengths[i] : 0u;
@@ -1257,12 +1326,23 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
     // the (message, part) of the one after are loaded a group ahead, and a
     // group's first two rounds are in flight before the previous group's
     // remainder reduction, move and combine run -- a wave's LDS slots are
-    // never idle while it computes.
-    uint32_t g = g0;
+    // never idle while it computes.  g is the group in hand, g1 the next
+    // (descriptors loading), g2 the one after (map entries loading); each
+    // new one is claimed from the block's counter, so a wave that runs
+    // faster takes more of the block's groups.
+    uint32_t g = gfirst, g1 = ngroups, g2 = ngroups;
     Group G;
     SegDesc nxt = {0ull, 0u, 0u, 0u, 0u};
     SegRef ref2 = {0u, 0u};
     if (g < ngroups) {
+#ifdef BMQCRC_EARLY_FIRST
+        if (identity) {  // A/B: the first group's loads before anything else
+            setup(spec, g, G);
+            issue_first_rounds(G);
+        }
+#endif
+        g1 = claim();
+        g2 = g1 < ngroups ? claim() : ngroups;
         const uint32_t s0 = g * 64u + (uint32_t)lane;
         SegRef r0 = {0u, 0u};
         if (!identity) {
@@ -1272,43 +1352,66 @@ __global__ __launch_bounds__(256, 2) void k_fold(BatchArgs a)
             }
         }
         const SegDesc d0 = identity ? spec : fetch_desc(a, r0, s0 < total);
-        const uint32_t s1 = (g + stride) * 64u + (uint32_t)lane;
-        const bool v1 = g + stride < ngroups && s1 < total;
+        const uint32_t s1 = g1 * 64u + (uint32_t)lane;
+        const bool v1 = g1 < ngroups && s1 < total;
         SegRef r1 = map_segment(a, &pl, s1, v1, identity, uni, sorted);
         if (sorted) {
             r1 = resolve_sorted(r1, v1);
         }
         nxt = fetch_desc(a, r1, v1);
-        const uint32_t s2 = (g + 2u * stride) * 64u + (uint32_t)lane;
-        ref2 = map_segment(a, &pl, s2, g + 2u * stride < ngroups && s2 < total, identity, uni,
-                           sorted);
-        setup(d0, g, G);
-        issue_first_rounds(G);
+        const uint32_t s2 = g2 * 64u + (uint32_t)lane;
+        ref2 = map_segment(a, &pl, s2, g2 < ngroups && s2 < total, identity, uni, sorted);
+#ifdef BMQCRC_EARLY_FIRST
+        if (!identity)
+#endif
+        {
+            setup(d0, g, G);
+            issue_first_rounds(G);
+        }
+        FOLD_STAMP(2)
     }
-    for (; g < ngroups; g += stride) {
+    bool first_group = true;
+    while (g < ngroups) {
         uint32_t Rm[32];
         fold_rounds(G, Rm);
+        if (first_group) {
+            FOLD_STAMP(3)
+            first_group = false;
+        }
+        if (g1 >= ngroups) {
+            FOLD_STAMP(4)
+        }
         // The slots are read: the next group's first rounds go out now, so
         // they load while this group's remainder is reduced and combined.
         const Group C = G;
-        if (g + stride < ngroups) {
+        uint32_t g3 = ngroups;
+        if (g1 < ngroups) {
             // setup first: it reads the descriptors loaded a group ago, and the
             // compiler's wait for them (which cannot see the DMA waits above)
             // must not also wait for the loads issued next
-            setup(nxt, g + stride, G);
-            const uint32_t s2 = (g + 2u * stride) * 64u + (uint32_t)lane;
-            const bool v2 = g + 2u * stride < ngroups && s2 < total;
+            setup(nxt, g1, G);
+            const uint32_t s2 = g2 * 64u + (uint32_t)lane;
+            const bool v2 = g2 < ngroups && s2 < total;
             nxt = fetch_desc(a, sorted ? resolve_sorted(ref2, v2) : ref2, v2);
-            const uint32_t s3 = (g + 3u * stride) * 64u + (uint32_t)lane;
-            ref2 = map_segment(a, &pl, s3, g + 3u * stride < ngroups && s3 < total, identity, uni,
-                               sorted);
+            g3 = g2 < ngroups ? claim() : ngroups;  // claims only grow: none left
+            const uint32_t s3 = g3 * 64u + (uint32_t)lane;
+            ref2 = map_segment(a, &pl, s3, g3 < ngroups && s3 < total, identity, uni, sorted);
             issue_first_rounds(G);
         }
         finish(C, C.hskip ? tail_horner<8>(Rm, tab_lds) : tail_horner(Rm, tab_lds));
+        g = g1;
+        g1 = g2;
+        g2 = g3;
     }
-    if (spec_mode && long_seen) {
-        second_pass();
+    FOLD_STAMP(5)
+    if (spec_mode) {
+        __syncthreads();  // the block's list of groups with skipped messages is complete
+        const uint32_t nlong = long_n;
+        if (nlong) {
+            second_pass(nlong);
+        }
     }
+    FOLD_STAMP(6)
 }
 
 // ---------------------------------------------------------------- planner
@@ -1824,6 +1927,9 @@ constexpr uint32_t kMapRegTiles = BMQCRC_MAP_REG_TILES;  // tiles kept in regist
                             // 1 no histogram atomics, 2 no last-segment claims, 4 no full-run
                             // writes, 8 no last-segment stores
 #endif
+#ifndef BMQCRC_PLAN_FLAGS
+#define BMQCRC_PLAN_FLAGS 0  // 1: round 3's separate arrival flags (A/B)
+#endif
 #ifndef BMQCRC_PLAN_DIAG
 #define BMQCRC_PLAN_DIAG 0  // 3: per-block phase stamps, 4: the same without seginfo stores,
                             // 6: every block's first read of the exchanged words is stale
@@ -2043,12 +2149,25 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             a.block_sum[lane * nb + bid] = wv;  // for k_fold (the next launch)
         }
+#if BMQCRC_PLAN_FLAGS
         __builtin_amdgcn_s_waitcnt(0);  // the stores above are complete (vmcnt 0)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if (lane == 0) {
             __hip_atomic_store(&sync[kSyncFlags + bid], (unsigned long long)ep, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
+        // poll the blocks' arrival flags
+        const unsigned long long* const arrive = sync + kSyncFlags;
+        constexpr int kArriveShift = 0;
+#else
+        // round 4: no separate flag.  The poll reads each block's tagged
+        // third block word (published beside its histogram, in no particular
+        // order: the tag check below re-reads any word still stale), so the
+        // wait for the stores' completion and the flag's own store and
+        // visibility latency are gone from the meeting.
+        const unsigned long long* const arrive = tags + kTagWords + 2u * kPlanMaxBlocks;
+        constexpr int kArriveShift = 32;
+#endif
         const uint64_t t0 = wall_clock64();
         uint32_t ok = 1u;
         static_assert(kPlanMaxBlocks <= 4 * 64, "four flags per lane");
@@ -2070,8 +2189,8 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
 #pragma unroll
             for (uint32_t k = 0; k < 4; ++k) {
                 const uint32_t b = (uint32_t)lane + 64u * k;
-                f[k] = b < nb ? __hip_atomic_load(&sync[kSyncFlags + b], __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT)
+                f[k] = b < nb ? __hip_atomic_load(&arrive[b], __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT) >> kArriveShift
                               : (unsigned long long)ep;
             }
             const unsigned long long gone =
@@ -2517,9 +2636,16 @@ extern "C" int bmqcrc_launch_batch(const BatchArgs* a, void* stream, int num_cus
         }
     }
     const uint64_t max_groups = (a->max_segs + 63) / 64;
-    uint64_t grid = (max_groups + kWavesPerBlock - 1) / kWavesPerBlock;
     const uint32_t per_cu = (a->tune & 2u) ? 1u : (a->tune & 8u) ? 2u : a->blocks_per_cu;
-    const uint64_t cap = (uint64_t)(num_cus > 0 ? num_cus : 256) * (per_cu ? per_cu : 2u);
+    const uint64_t cus = (uint64_t)(num_cus > 0 ? num_cus : 256);
+    // Two waves per SIMD as ONE block of 8 waves per CU whose waves claim
+    // the block's groups dynamically, when the batch gives every wave at
+    // least two groups; otherwise (one wave per SIMD, or small batches that
+    // should reach more CUs) 4-wave blocks, per_cu of them per CU.
+    const bool wide = per_cu == 2u && !(a->tune & 1024u) && max_groups >= 2u * 8u * cus;
+    const uint32_t wpb = wide ? 8u : 4u;
+    uint64_t grid = (max_groups + wpb - 1) / wpb;
+    const uint64_t cap = wide ? cus : cus * (per_cu ? per_cu : 2u);
     if (grid > cap) {
         grid = cap;
     }
@@ -2530,17 +2656,23 @@ extern "C" int bmqcrc_launch_batch(const BatchArgs* a, void* stream, int num_cus
         (void)hipEventRecord((hipEvent_t)ev_start, s);
     }
     const bool one = a->spec == 1u && !a->whole && !(a->tune & 64u);
-    if (!(a->tune & 1u)) {  // default: non-temporal LDS-DMA (once-read stream)
-        if (one) {
-            hipLaunchKernelGGL((k_fold<true, true>), dim3((unsigned)grid),
-                               dim3(kWavesPerBlock * 64), 0, s, *a);
+    const dim3 gd((unsigned)grid), bd(wpb * 64u);
+    if (a->tune & 1u) {  // A/B: default-policy LDS-DMA for long streams too
+        if (wide) {
+            hipLaunchKernelGGL((k_fold<false, false, 8>), gd, bd, 0, s, *a);
         } else {
-            hipLaunchKernelGGL((k_fold<true, false>), dim3((unsigned)grid),
-                               dim3(kWavesPerBlock * 64), 0, s, *a);
+            hipLaunchKernelGGL((k_fold<false, false, 4>), gd, bd, 0, s, *a);
         }
+    } else if (one) {  // default: non-temporal LDS-DMA for long streams (once-read)
+        if (wide) {
+            hipLaunchKernelGGL((k_fold<true, true, 8>), gd, bd, 0, s, *a);
+        } else {
+            hipLaunchKernelGGL((k_fold<true, true, 4>), gd, bd, 0, s, *a);
+        }
+    } else if (wide) {
+        hipLaunchKernelGGL((k_fold<true, false, 8>), gd, bd, 0, s, *a);
     } else {
-        hipLaunchKernelGGL((k_fold<false, false>), dim3((unsigned)grid),
-                           dim3(kWavesPerBlock * 64), 0, s, *a);
+        hipLaunchKernelGGL((k_fold<true, false, 4>), gd, bd, 0, s, *a);
     }
     if (ev_stop) {
         (void)hipEventRecord((hipEvent_t)ev_stop, s);
@@ -2558,6 +2690,15 @@ extern "C" int bmqcrc_plan_map_occupancy(int* blocks_per_cu)
     *blocks_per_cu = per;
     return 0;
 }
+
+#if BMQCRC_FOLD_DIAG
+extern "C" __attribute__((visibility("default"))) int bmqcrc_diag_fold_trace(unsigned long long* out)
+{
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fold_trace), sizeof(g_fold_trace)) == hipSuccess
+               ? 0
+               : -5;
+}
+#endif
 
 #if BMQCRC_PLAN_DIAG >= 3
 extern "C" __attribute__((visibility("default"))) int bmqcrc_diag_plan_trace(unsigned long long* out)

@@ -306,6 +306,19 @@ def test_config_1k_x_4KiB_planned_then_speculative(cuda):
     forget_shape(cuda.index, s)
     assert run()["spec"] == 0                   # planned again, then speculative again
     assert run()["spec"] == 16
+    # with the prediction dropped, a declared length range that has one
+    # uniform segment count (bmqcrc_opts.min_len / max_len, ABI 2.5) is the
+    # same single launch, no planner and no history needed
+
+    def declared():
+        got = Crc32c.calculate_batch(arena, o, ln, stream=s, max_len=size, min_len=size)
+        s.synchronize()
+        assert np.array_equal(got.cpu().numpy().view(np.uint32), exp)
+        return last_launch(cuda.index, s)
+
+    for _ in range(3):
+        forget_shape(cuda.index, s)
+        assert declared() == {"kernels": 1, "spec": 16, "seg_bytes": 256}
 
 
 def test_config_1M_x_256B_full(cuda):
