@@ -63,6 +63,9 @@ struct BatchArgs {
     uint32_t* seginfo;         // workspace, max_segs: segments in size-class order, one word
                                // each (message, | kSegLast for its last segment)
     uint32_t* firstk;          // workspace, max_segs / 64 + 1: k of each group's first entry
+    unsigned long long* gdesc; // workspace, max_segs / 64 + 2 (round 4): (epoch << 32) | message
+                               // for a group whose 64 seginfo slots are all full segments of
+                               // one message (k_plan_map writes this instead of the 64 entries)
     uint32_t* bhist;           // workspace, kBuckets * nblocks: per-block size-class histogram
     uint64_t n;
     uint64_t max_segs;

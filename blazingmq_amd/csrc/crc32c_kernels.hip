@@ -510,6 +510,11 @@ __device__ __forceinline__ void dma_round(uint32_t lds_dst, const uint64_t (&pba
         : "memory", "scc");
 }
 
+#ifndef BMQCRC_GROUP_DESC
+#define BMQCRC_GROUP_DESC 1  // 0: every seginfo entry written (round 3; A/B)
+#endif
+constexpr bool kGroupDesc = BMQCRC_GROUP_DESC != 0;
+
 // Planner words every consumer block keeps in LDS (filled by plan_totals):
 // the exclusive segment offset of each k_plan block and its common segment
 // count per message (~0 when its messages differ).
@@ -778,8 +783,17 @@ __device__ __forceinline__ SegRef map_segment(const BatchArgs& a, const PlanLds*
             r.k = seg - r.msg * uni;
         } else {
             // sorted: the raw entry and its group's firstk (resolved in fetch_desc)
+            const uint32_t gsel = (uint32_t)__builtin_amdgcn_readfirstlane((int)seg) >> 6;
             r.msg = a.seginfo[seg];
-            r.k = a.firstk[(uint32_t)__builtin_amdgcn_readfirstlane((int)seg) >> 6];
+            r.k = a.firstk[gsel];
+            if (kGroupDesc) {
+                // a group of 64 full segments of one message: one tagged word
+                // instead of its 64 entries (which are then not written)
+                const unsigned long long gd = a.gdesc[gsel];
+                if ((uint32_t)(gd >> 32) == a.plan_epoch) {
+                    r.msg = (uint32_t)gd;
+                }
+            }
         }
     }
     return r;
@@ -918,8 +932,9 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
         __builtin_amdgcn_s_setprio(BMQCRC_LATE_PRIO);
     }
 #endif
-    // the wave's first group (claim k = wave), as if segment = message
-    const uint32_t gfirst = blockIdx.x + wave * gridDim.x;
+    // the wave's first group (claim k = wave, see gid below), as if
+    // segment = message
+    const uint32_t gfirst = blockIdx.x * WPB + wave;
     const uint32_t sid = gfirst * 64u + (uint32_t)lane;
     const SegDesc spec = fetch_desc(a, SegRef{sid, 0u}, sid < a.n);
     // remainder-reduction tables -> LDS (8 KiB, once per block; no DMA in
@@ -994,15 +1009,29 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     const uint32_t rd_off = (uint32_t)lane * 128u + (((uint32_t)lane >> 1) & 7u) * 16u;
     const uint64_t zero = (uint64_t)(uintptr_t)g_zero_line + 16u * ((uint32_t)lane & 7u);
 
-    // claim k of this block = group blockIdx.x + k gridDim.x (>= ngroups: none)
+    // Claim k of this block is group WPB (blockIdx.x + G (k / WPB)) + k % WPB
+    // (G = gridDim.x; >= ngroups: none): the groups round 3's grid-stride
+    // waves of this block took, so one-group-per-wave batches keep their
+    // layout -- a block's first WPB groups are adjacent in memory (mapping
+    // claim k to group blockIdx.x + G k instead cost the headline 1.5-2 %,
+    // profiles/r04/ab/)
     const uint32_t nbk = gridDim.x;
-    auto claim = [&]() {
+    auto gid = [&](uint32_t k) {
+        return (blockIdx.x + nbk * (k / (uint32_t)WPB)) * (uint32_t)WPB + k % (uint32_t)WPB;
+    };
+    // a claim in two halves: the LDS atomic (lane 0) is issued early and its
+    // result read later, so its latency hides behind other LDS work
+    auto claim_issue = [&]() {
         uint32_t k = 0;
         if (lane == 0) {
             k = atomicAdd(&claim_ctr, 1u);
         }
-        return blockIdx.x + (uint32_t)__builtin_amdgcn_readfirstlane((int)k) * nbk;
+        return k;
     };
+    auto claim_take = [&](uint32_t k) {
+        return gid((uint32_t)__builtin_amdgcn_readfirstlane((int)k));
+    };
+    auto claim = [&]() { return claim_take(claim_issue()); };
     const uint32_t seg_shift = (SEG & (SEG - 1u)) == 0 ? (uint32_t)__builtin_ctz(SEG) : 0u;
 
     // One group = 64 segments, one per lane.  Its per-lane geometry and the
@@ -1280,7 +1309,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
         const uint32_t mpg = 64u / spec_u;  // messages per group
         const bool listed = nlong <= kLongListCap;
         for (uint32_t j = wave;; j += WPB) {
-            const uint32_t gg = listed ? (j < nlong ? long_list[j] : ngroups) : blockIdx.x + j * nbk;
+            const uint32_t gg = listed ? (j < nlong ? long_list[j] : ngroups) : gid(j);
             if (gg >= ngroups) {
                 break;
             }
@@ -1372,6 +1401,10 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     }
     bool first_group = true;
     while (g < ngroups) {
+        // the claim of the group after g2, issued before this group's fold
+        // (whose LDS reads cover the atomic's latency), taken below
+        const bool more = g1 < ngroups && g2 < ngroups;  // claims only grow: none left
+        const uint32_t k3 = more ? claim_issue() : 0u;
         uint32_t Rm[32];
         fold_rounds(G, Rm);
         if (first_group) {
@@ -1393,7 +1426,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
             const uint32_t s2 = g2 * 64u + (uint32_t)lane;
             const bool v2 = g2 < ngroups && s2 < total;
             nxt = fetch_desc(a, sorted ? resolve_sorted(ref2, v2) : ref2, v2);
-            g3 = g2 < ngroups ? claim() : ngroups;  // claims only grow: none left
+            g3 = more ? claim_take(k3) : ngroups;
             const uint32_t s3 = g3 * 64u + (uint32_t)lane;
             ref2 = map_segment(a, &pl, s3, g3 < ngroups && s3 < total, identity, uni, sorted);
             issue_first_rounds(G);
@@ -2408,7 +2441,24 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
                     const uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)nf[v], src);
                     if (n > kMapShortRun) {
                         const uint32_t i = (uint32_t)(wbase + (uint32_t)src * kPlanV + v);
-                        for (uint32_t k = (uint32_t)lane; k < n; k += 64u) {
+                        // groups wholly inside [at2, at2 + n): one tagged
+                        // descriptor each (and its firstk) instead of 64
+                        // entries; the entries of the partial groups at
+                        // either end as before
+                        const uint32_t gf = (at2 + 63u) >> 6, ge = (at2 + n) >> 6;
+                        const uint32_t kh = kGroupDesc && gf < ge ? 64u * gf - at2 : n;
+                        const uint32_t kt = kGroupDesc && gf < ge ? 64u * ge - at2 : n;
+                        for (uint32_t k = (uint32_t)lane; k < kh; k += 64u) {
+                            put_full(a, at2 + k, i, k);
+                        }
+                        if (kGroupDesc) {
+                            const unsigned long long tag = (unsigned long long)ep << 32 | i;
+                            for (uint32_t g = gf + (uint32_t)lane; g < ge; g += 64u) {
+                                a.gdesc[g] = tag;
+                                a.firstk[g] = 64u * g - at2;
+                            }
+                        }
+                        for (uint32_t k = kt + (uint32_t)lane; k < n; k += 64u) {
                             put_full(a, at2 + k, i, k);
                         }
                         at2 += n;
