@@ -10,7 +10,7 @@ waves start, their prologue (tables, planner words), the first descriptors
 -> DMA issue, the first group's data landing and fold, the loop, the last
 group's remainder and combine, and where the launch ends.
 
-  usage: python3 tools/fold_trace_diag.py <config> [msgs] [msg_bytes] [raw.npy]
+  usage: python3 tools/fold_trace_diag.py <config | zipf_4M[:i/N]> [msgs] [msg_bytes] [raw.npy]
 """
 import ctypes
 import json
@@ -29,16 +29,27 @@ def main():
     import blazingmq_amd as bmq
     from blazingmq_amd import Crc32c, _native
     cfg = sys.argv[1] if len(sys.argv) > 1 else "1M_x_256B"
-    size = int(sys.argv[3]) if len(sys.argv) > 3 else bench.UNIFORM_SIZES[cfg]
-    n = int(sys.argv[2]) if len(sys.argv) > 2 else len(bench.CONFIGS[cfg][1](0, 1)[0])
     dev = torch.device("cuda", 0)
-    arena = torch.empty(n * size + 64, dtype=torch.uint8, device=dev)
-    bmq.fill_synthetic(arena, 1)
-    o = torch.arange(n, dtype=torch.int64, device=dev) * size
-    ln = torch.full((n,), size, dtype=torch.int32, device=dev)
+    if cfg.startswith("zipf"):  # zipf_4M or zipf_4M:i/N (one strong-scaling shard)
+        si, sn = (int(x) for x in (cfg.split(":")[1] if ":" in cfg else "0/1").split("/"))
+        lens, begin = bench._zipf(si, sn)
+        n, size = int(lens.size), 0
+        offs = np.zeros(n, dtype=np.int64)
+        np.cumsum(lens[:-1], dtype=np.int64, out=offs[1:])
+        arena = torch.empty(int(lens.sum(dtype=np.uint64)) + 64, dtype=torch.uint8, device=dev)
+        bmq.fill_synthetic(arena, 4, begin=begin)
+        o = torch.from_numpy(offs).to(dev)
+        ln = torch.from_numpy(lens.view(np.int32)).to(dev)
+    else:
+        size = int(sys.argv[3]) if len(sys.argv) > 3 else bench.UNIFORM_SIZES[cfg]
+        n = int(sys.argv[2]) if len(sys.argv) > 2 else len(bench.CONFIGS[cfg][1](0, 1)[0])
+        arena = torch.empty(n * size + 64, dtype=torch.uint8, device=dev)
+        bmq.fill_synthetic(arena, 1)
+        o = torch.arange(n, dtype=torch.int64, device=dev) * size
+        ln = torch.full((n,), size, dtype=torch.int32, device=dev)
     out = torch.empty(n, dtype=torch.int32, device=dev)
     s = torch.cuda.current_stream(dev)
-    for _ in range(50):
+    for _ in range(50 if size else 8):
         Crc32c.calculate_batch(arena, o, ln, None, out, stream=s, sync=False)
     torch.cuda.synchronize()
     kw = 4096
