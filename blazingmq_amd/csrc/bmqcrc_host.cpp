@@ -275,10 +275,9 @@ int plan_ws(Workspace* w, hipStream_t s, uint64_t n, uint64_t arena_bytes, uint3
     if (w->gdesc.fresh) {  // no group descriptor of any epoch (epochs start at 1)
         HIP_TRY(hipMemsetAsync(w->gdesc.p, 0, w->gdesc.bytes, s));
     }
-    w->plan_epoch = w->plan_epoch + 1u;
-    if (w->plan_epoch == 0) {
-        w->plan_epoch = 1;
-    }
+    // host tags stay in [1, 2^31): a batch captured into a graph takes its
+    // tags from the device instead (0x80000000 | count, k_epoch_advance)
+    w->plan_epoch = w->plan_epoch % 0x7fffffffu + 1u;
     a->plan_sync = (unsigned long long*)w->plan_sync.p;
     a->plan_epoch = w->plan_epoch;
     a->map_wait_ticks = w->map_wait_ticks;
@@ -489,6 +488,14 @@ int run_batch(Ctx& c, uint32_t flags, uint32_t seg, const void* arena, uint64_t 
         if (w->pair_left) {
             a.pair = 1;
             --w->pair_left;
+        }
+    }
+    if (!a.whole && !a.spec && a.map_planned) {
+        // inside a graph capture every replay must tag its planner words
+        // afresh: the tag then lives on the device (BatchArgs::plan_epoch 0)
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(c.s, &cap) == hipSuccess && cap == hipStreamCaptureStatusActive) {
+            a.plan_epoch = 0;
         }
     }
     a.arena = (const uint8_t*)arena;

@@ -91,14 +91,16 @@ struct BatchArgs {
     // segments at a time -- correct for any batch, only slower when the
     // guess was wrong.
     uint32_t spec;
-    // Single-pass planner (k_plan_map): [2] the epoch of a launch whose map
+    // Single-pass planner (k_plan_map): [1] the device-side launch tag of
+    // graph-captured batches, [2] the epoch of a launch whose map
     // was given up (k_fold then searches seg_first), [3] how many
     // launches gave theirs up, [kSyncFlags + b] block b's arrival flag (the
     // epoch of the launch it last arrived in), then kPlanMaxBlocks x
     // (kBuckets + 3) epoch-tagged words the blocks exchange.  Zeroed once
     // when allocated.
     unsigned long long* plan_sync;
-    uint32_t plan_epoch;       // k_plan_map launch tag on this workspace, never 0
+    uint32_t plan_epoch;       // k_plan_map launch tag on this workspace, in [1, 2^31); 0: the
+                               // tag is plan_sync[1], advanced on the device (graph capture)
     uint64_t map_wait_ticks;   // k_plan_map's grid-wide wait limit (100 MHz wall clock)
     uint32_t class_desc;       // k_plan_map: size classes in descending order (short schedules)
     // 1: plan this ragged batch with the meeting-free pair k_plan<true> +

@@ -515,6 +515,23 @@ __device__ __forceinline__ void dma_round(uint32_t lds_dst, const uint64_t (&pba
 #endif
 constexpr bool kGroupDesc = BMQCRC_GROUP_DESC != 0;
 
+// The single-pass planner's launch tag.  Normally the host's per-workspace
+// count (BatchArgs::plan_epoch, below 2^31); a batch captured into a graph
+// gets 0 there and takes the tag from the device word plan_sync[1], which
+// k_epoch_advance moves on before every planner launch -- so every replay
+// tags its words afresh (a frozen argument would let one replay read the
+// previous replay's histogram as current).
+__device__ __forceinline__ uint32_t launch_epoch(const BatchArgs& a)
+{
+    return a.plan_epoch ? a.plan_epoch : (uint32_t)a.plan_sync[1];
+}
+
+__global__ void k_epoch_advance(unsigned long long* sync)
+{
+    const unsigned long long e = sync[1];
+    sync[1] = 0x80000000ull | ((e + 1ull) & 0x7fffffffull);  // never 0, disjoint from host tags
+}
+
 // Planner words every consumer block keeps in LDS (filled by plan_totals):
 // the exclusive segment offset of each k_plan block and its common segment
 // count per message (~0 when its messages differ).
@@ -759,7 +776,7 @@ struct SegDesc {
 
 __device__ __forceinline__ SegRef map_segment(const BatchArgs& a, const PlanLds* pl,
                                               uint32_t seg, bool valid, uint32_t identity,
-                                              uint32_t uni, uint32_t sorted)
+                                              uint32_t uni, uint32_t sorted, uint32_t ep)
 {
     SegRef r = {0u, 0u};
     if (!identity && !uni && !sorted) {
@@ -790,7 +807,7 @@ __device__ __forceinline__ SegRef map_segment(const BatchArgs& a, const PlanLds*
                 // a group of 64 full segments of one message: one tagged word
                 // instead of its 64 entries (which are then not written)
                 const unsigned long long gd = a.gdesc[gsel];
-                if ((uint32_t)(gd >> 32) == a.plan_epoch) {
+                if ((uint32_t)(gd >> 32) == ep) {
                     r.msg = (uint32_t)gd;
                 }
             }
@@ -913,10 +930,12 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     const uint32_t spec_u = spec_mode ? spec_mode : 1u;
     PlanWords pw = {0u, 0u, 0u, 0u};
     uint32_t map_void = 0u;  // k_plan_map gave up its map for this launch
+    uint32_t ep = a.plan_epoch;  // the planner's launch tag (0: kept on the device)
     if (!whole && !spec_mode) {
         pw = plan_load(a);
         if (a.map_planned && a.plan_sync) {
-            map_void = (uint32_t)a.plan_sync[2] == a.plan_epoch;
+            ep = launch_epoch(a);
+            map_void = (uint32_t)a.plan_sync[2] == ep;
         }
     }
     // x^(-8p) un-shift table -> LDS too: a per-lane index, so from constant
@@ -1000,7 +1019,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
                                                   : kHintRagged,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (map_void) {  // the GPU was shared: the host plans with the pair for a while
-            __hip_atomic_store(a.shape_hint + 1, a.plan_epoch, __ATOMIC_RELAXED,
+            __hip_atomic_store(a.shape_hint + 1, ep, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
@@ -1375,7 +1394,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
         const uint32_t s0 = g * 64u + (uint32_t)lane;
         SegRef r0 = {0u, 0u};
         if (!identity) {
-            r0 = map_segment(a, &pl, s0, s0 < total, identity, uni, sorted);
+            r0 = map_segment(a, &pl, s0, s0 < total, identity, uni, sorted, ep);
             if (sorted) {
                 r0 = resolve_sorted(r0, s0 < total);
             }
@@ -1383,13 +1402,13 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
         const SegDesc d0 = identity ? spec : fetch_desc(a, r0, s0 < total);
         const uint32_t s1 = g1 * 64u + (uint32_t)lane;
         const bool v1 = g1 < ngroups && s1 < total;
-        SegRef r1 = map_segment(a, &pl, s1, v1, identity, uni, sorted);
+        SegRef r1 = map_segment(a, &pl, s1, v1, identity, uni, sorted, ep);
         if (sorted) {
             r1 = resolve_sorted(r1, v1);
         }
         nxt = fetch_desc(a, r1, v1);
         const uint32_t s2 = g2 * 64u + (uint32_t)lane;
-        ref2 = map_segment(a, &pl, s2, g2 < ngroups && s2 < total, identity, uni, sorted);
+        ref2 = map_segment(a, &pl, s2, g2 < ngroups && s2 < total, identity, uni, sorted, ep);
 #ifdef BMQCRC_EARLY_FIRST
         if (!identity)
 #endif
@@ -1428,7 +1447,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
             nxt = fetch_desc(a, sorted ? resolve_sorted(ref2, v2) : ref2, v2);
             g3 = more ? claim_take(k3) : ngroups;
             const uint32_t s3 = g3 * 64u + (uint32_t)lane;
-            ref2 = map_segment(a, &pl, s3, g3 < ngroups && s3 < total, identity, uni, sorted);
+            ref2 = map_segment(a, &pl, s3, g3 < ngroups && s3 < total, identity, uni, sorted, ep);
             issue_first_rounds(G);
         }
         finish(C, C.hskip ? tail_horner<8>(Rm, tab_lds) : tail_horner(Rm, tab_lds));
@@ -2001,7 +2020,7 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
     __shared__ uint32_t go;
     __shared__ PlanTail tail;
     __shared__ uint32_t sruns[kPlanBlock / 64][64 * kPlanV];  // per wave: short-run ends
-    const uint32_t nb = a.nblocks, ep = a.plan_epoch, bid = blockIdx.x;
+    const uint32_t nb = a.nblocks, ep = launch_epoch(a), bid = blockIdx.x;
     load_tail(a, min((uint64_t)bid * a.per_msg + a.per_msg, a.n), true, &tail);
     // epoch-tagged words the blocks exchange (plan_sync after the flags),
     // laid out for coalesced reads: [c * kPlanMaxBlocks + b] histograms,
@@ -2665,6 +2684,9 @@ extern "C" int bmqcrc_launch_batch(const BatchArgs* a, void* stream, int num_cus
     hipStream_t s = (hipStream_t)stream;
     if (a->n == 0) {
         return 0;
+    }
+    if (!a->whole && !a->spec && a->map_planned && single_pass_planner(*a) && a->plan_epoch == 0) {
+        hipLaunchKernelGGL(k_epoch_advance, dim3(1), dim3(1), 0, s, a->plan_sync);
     }
     if (!a->whole && !a->spec) {
         // Ragged batch expected: the single-pass planner when its blocks

@@ -53,6 +53,54 @@ def test_graph_capture_and_replay(cuda, whole):
         assert np.array_equal(got, oracle.batch(new, offs, lens, seeds, nthreads=8)), it
 
 
+def test_graph_replays_of_a_ragged_batch_with_new_lengths(cuda):
+    # A planned ragged batch captured into a graph, replayed with new lengths,
+    # offsets and payload each time (the device arrays rewritten in place).
+    # The single-pass planner tags the words its blocks exchange with the
+    # launch's epoch; captured, that tag lives on the device and advances on
+    # every replay (k_epoch_advance), so no replay reads the previous one's
+    # histogram or group descriptors as current.
+    import torch
+    from blazingmq_amd import last_launch
+    rng = np.random.default_rng(35)
+    size, n = 48 << 20, 200_000
+    side = torch.cuda.Stream(cuda)
+    arena = torch.zeros(size, dtype=torch.uint8, device=cuda)
+    o = torch.zeros(n, dtype=torch.int64, device=cuda)
+    ln = torch.zeros(n, dtype=torch.int32, device=cuda)
+    out = torch.zeros(n, dtype=torch.int32, device=cuda)
+    reserve(cuda.index or 0, side, n, size, 2048)
+
+    def new_batch():
+        lens = np.concatenate([rng.integers(0, 300, size=n - 400),
+                               rng.integers(0, 60000, size=400)]).astype(np.uint32)
+        rng.shuffle(lens)
+        offs = (rng.random(n) * (size - lens + 1)).astype(np.int64)
+        data = rng.integers(0, 256, size=size, dtype=np.uint8)
+        arena.copy_(torch.from_numpy(data).to(cuda))
+        o.copy_(torch.from_numpy(offs).to(cuda))
+        ln.copy_(torch.from_numpy(lens.view(np.int32)).to(cuda))
+        torch.cuda.synchronize()
+        return oracle.batch(data, offs, lens, None, nthreads=8)
+
+    exp = new_batch()
+    with torch.cuda.stream(side):  # warm: the workspace learns the batch is ragged
+        Crc32c.calculate_batch(arena, o, ln, None, out, stream=side, sync=False, seg_bytes=2048)
+    side.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), exp)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        Crc32c.calculate_batch(arena, o, ln, None, out, stream=side, sync=False, seg_bytes=2048)
+    assert last_launch(cuda.index or 0, side)["kernels"] == 2  # k_plan_map + k_fold captured
+    for it in range(4):
+        exp = new_batch()
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        bad = np.nonzero(out.cpu().numpy().view(np.uint32) != exp)[0]
+        assert bad.size == 0, (it, bad[:8])
+
+
 def test_concurrent_streams_and_threads(cuda):
     import torch
     rng = np.random.default_rng(41)
