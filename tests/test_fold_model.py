@@ -460,3 +460,48 @@ def test_last_segment_class():
         _, nl = geom(S, E, k == 0)
         assert last_class_nl(off & 0xFFFFFFFF, ln, seg) == nl, (off, ln, seg)
 
+
+
+def _find_msg_group(first, n, s0, lane_segs):
+    """Python restatement of k_fold's find_msg_group (crc32c_kernels.hip):
+    one search for the group's first segment s0, then the window of the next
+    64 messages' first segments and a 6-step search per lane; a lane past the
+    window searches on its own.  first[i] = exclusive prefix of segment
+    counts (message i's first segment), len n."""
+    import bisect
+    m0 = bisect.bisect_right(first, s0) - 1           # last i with first[i] <= s0
+    w = [first[m0 + j] if m0 + j < n else 0xFFFFFFFF for j in range(64)]
+    w64 = first[m0 + 64] if m0 + 64 < n else 0xFFFFFFFF
+    out = []
+    for seg in lane_segs:
+        j = 0
+        for st in (32, 16, 8, 4, 2, 1):
+            if w[j + st] <= seg:
+                j += st
+        msg, f = m0 + j, w[j]
+        if j == 63 and w64 <= seg:
+            msg = bisect.bisect_right(first, seg) - 1
+            f = first[msg]
+        out.append((msg, seg - f))
+    return out
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_group_search_maps_every_segment(seed):
+    """The given-up map's segment search (round 4) against a brute-force map
+    over batches with empty messages (zero segments) in runs, long messages
+    and groups spanning more than 64 messages."""
+    rng = np.random.default_rng(seed)
+    n = 3000
+    kinds = rng.integers(0, 4, size=n)
+    segs = np.where(kinds == 0, 0, np.where(kinds == 1, 1, rng.integers(1, 90, size=n)))
+    if seed % 2:
+        segs[100:400] = 0                               # a long run of empty messages
+    first = np.concatenate([[0], np.cumsum(segs)[:-1]]).astype(np.int64).tolist()
+    total = int(segs.sum())
+    owner = np.repeat(np.arange(n), segs)
+    kidx = np.concatenate([np.arange(s) for s in segs if s]) if total else np.zeros(0, int)
+    for g in range((total + 63) // 64):
+        lanes = [s for s in range(64 * g, min(64 * g + 64, total))]
+        got = _find_msg_group(first, n, 64 * g, lanes)
+        assert got == [(int(owner[s]), int(kidx[s])) for s in lanes], g
