@@ -335,6 +335,7 @@ __device__ __forceinline__ uint32_t tab_lookup(uint32_t tab_lds, int k, uint32_t
     return *(const lds_u32*)(uintptr_t)(tab_lds + k * 1024u + b * 4u);
 }
 
+
 // The last round's taps into the previous round (d + k <= 31): R_d = m_d ^
 // H_d.  A pair (k, k+1) with d + k + 1 <= 31 is p[d + k].
 __device__ __forceinline__ void tail_taps(const uint32_t (&q)[32], const uint32_t (&p)[32],
@@ -866,11 +867,6 @@ __device__ unsigned long long g_fold_trace[kFoldTraceWaves][8];
 #define FOLD_STAMP(k)
 #endif
 
-#ifndef BMQCRC_RR_SORTED
-#define BMQCRC_RR_SORTED 1  // 0: sorted maps keep the 8-group block chunks (A/B)
-#endif
-constexpr bool kRoundRobinSorted = BMQCRC_RR_SORTED != 0;
-
 // Groups whose speculative first pass skipped a message (a block's list for
 // the second pass; past this many the second pass scans the block's groups).
 constexpr uint32_t kLongListCap = 64;
@@ -1038,20 +1034,11 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     // waves of this block took, so one-group-per-wave batches keep their
     // layout -- a block's first WPB groups are adjacent in memory (mapping
     // claim k to group blockIdx.x + G k instead cost the headline 1.5-2 %,
-    // profiles/r04/ab/)
-    //
-    // A size-class-sorted map interleaves single groups instead (claim k =
-    // group blockIdx.x + G k): with 8-group chunks per block, a class whose
-    // group count is not a multiple of 8 G left some blocks a whole chunk --
-    // one more of its groups per wave -- and the launch ended on them (the
-    // 1/8 Zipf shard's blocks finished 475-534 us apart,
-    // profiles/r04/fold_trace/).  Sorted order carries no memory adjacency
-    // to keep.
+    // profiles/r04/ab/; interleaving single groups for size-class-sorted
+    // maps measured the same as these chunks, profiles/r04/ab/rr/)
     const uint32_t nbk = gridDim.x;
-    const bool rr = kRoundRobinSorted && sorted;
     auto gid = [&](uint32_t k) {
-        return rr ? blockIdx.x + nbk * k
-                  : (blockIdx.x + nbk * (k / (uint32_t)WPB)) * (uint32_t)WPB + k % (uint32_t)WPB;
+        return (blockIdx.x + nbk * (k / (uint32_t)WPB)) * (uint32_t)WPB + k % (uint32_t)WPB;
     };
     // a claim in two halves: the LDS atomic (lane 0) is issued early and its
     // result read later, so its latency hides behind other LDS work
@@ -1393,7 +1380,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     // (descriptors loading), g2 the one after (map entries loading); each
     // new one is claimed from the block's counter, so a wave that runs
     // faster takes more of the block's groups.
-    uint32_t g = gid(wave), g1 = ngroups, g2 = ngroups;  // (= gfirst unless rr)
+    uint32_t g = gid(wave), g1 = ngroups, g2 = ngroups;  // (= gfirst)
     Group G;
     SegDesc nxt = {0ull, 0u, 0u, 0u, 0u};
     SegRef ref2 = {0u, 0u};
@@ -1994,9 +1981,6 @@ constexpr uint32_t kMapRegTiles = BMQCRC_MAP_REG_TILES;  // tiles kept in regist
                             // 1 no histogram atomics, 2 no last-segment claims, 4 no full-run
                             // writes, 8 no last-segment stores
 #endif
-#ifndef BMQCRC_LAST_AGG
-#define BMQCRC_LAST_AGG 0  // 1: last-segment claims aggregated per class and wave (A/B)
-#endif
 #ifndef BMQCRC_PLAN_FLAGS
 #define BMQCRC_PLAN_FLAGS 0  // 1: round 3's separate arrival flags (A/B)
 #endif
@@ -2505,34 +2489,6 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
 #endif
         }
         // last (or only) segments: one returning LDS atomic per message
-#if BMQCRC_LAST_AGG
-        // A/B: one atomic per distinct class present in the wave (lanes of
-        // one class share it; Zipf's skew puts half the messages in class 0)
-#pragma unroll
-        for (uint32_t v = 0; v < kPlanV; ++v) {
-            const uint32_t c = (cls >> (8u * v)) & 0xffu;
-            const uint64_t below = (1ull << lane) - 1ull;
-            uint32_t at = 0;
-            for (uint64_t todo = __ballot(c < (uint32_t)kBuckets); todo;) {
-                const int leader = __builtin_ctzll(todo);
-                const uint32_t cl = (uint32_t)__builtin_amdgcn_readlane((int)c, leader);
-                const uint64_t same = __ballot(c == cl);
-                uint32_t b = 0;
-                if (lane == leader) {
-                    b = atomicAdd(&run[cl], (uint32_t)__popcll(same));
-                }
-                b = (uint32_t)__builtin_amdgcn_readlane((int)b, leader);
-                if (c == cl) {
-                    at = b + (uint32_t)__popcll(same & below);
-                }
-                todo &= ~same;
-            }
-            if (c < (uint32_t)kBuckets) {
-                put_last(a, at, (uint32_t)(base + (uint64_t)threadIdx.x * kPlanV + v));
-            }
-        }
-        if (false)
-#endif
 #pragma unroll
         for (uint32_t v = 0; v < kPlanV; ++v) {
             const uint32_t c = (cls >> (8u * v)) & 0xffu;
