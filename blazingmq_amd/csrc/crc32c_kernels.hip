@@ -945,13 +945,6 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     const uint32_t xn = threadIdx.x < 136u ? c_xneg8[threadIdx.x] : 0u;
     [[maybe_unused]] const uint32_t g0 = blockIdx.x * WPB + wave;  // this wave's index in the grid
     FOLD_STAMP(0)
-#ifdef BMQCRC_LATE_PRIO
-    // A/B: the second half of the grid (the second block of each CU) at a
-    // raised issue priority
-    if (blockIdx.x >= gridDim.x / 2) {
-        __builtin_amdgcn_s_setprio(BMQCRC_LATE_PRIO);
-    }
-#endif
     // the wave's first group (claim k = wave, see gid below), as if
     // segment = message
     const uint32_t gfirst = blockIdx.x * WPB + wave;
@@ -1385,12 +1378,6 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     SegDesc nxt = {0ull, 0u, 0u, 0u, 0u};
     SegRef ref2 = {0u, 0u};
     if (g < ngroups) {
-#ifdef BMQCRC_EARLY_FIRST
-        if (identity) {  // A/B: the first group's loads before anything else
-            setup(spec, g, G);
-            issue_first_rounds(G);
-        }
-#endif
         g1 = claim();
         g2 = g1 < ngroups ? claim() : ngroups;
         const uint32_t s0 = g * 64u + (uint32_t)lane;
@@ -1411,13 +1398,8 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
         nxt = fetch_desc(a, r1, v1);
         const uint32_t s2 = g2 * 64u + (uint32_t)lane;
         ref2 = map_segment(a, &pl, s2, g2 < ngroups && s2 < total, identity, uni, sorted, ep);
-#ifdef BMQCRC_EARLY_FIRST
-        if (!identity)
-#endif
-        {
-            setup(d0, g, G);
-            issue_first_rounds(G);
-        }
+        setup(d0, g, G);
+        issue_first_rounds(G);
         FOLD_STAMP(2)
     }
     bool first_group = true;
