@@ -672,32 +672,36 @@ __device__ PlanTotals plan_reduce(const BatchArgs& a, PlanLds* pl, const PlanWor
     const uint32_t v = w.v, nn = w.nn, u = w.u, u0 = w.u0;
     PlanTotals t;
     t.overflow = 0u;
-    // Closed forms need no offsets: one barrier for identity, two for uniform.
-    const int ragged = __syncthreads_or(nn != 0u);
-    if (!ragged) {  // every message exactly one segment
+    // One barrier for the shape, a second for the block offsets: each wave
+    // reduces its words by DPP and ballots (a chain of LDS round trips
+    // before) and publishes its sum and flags; every thread then combines
+    // the waves' entries.  (A block over the limit stores ~0 segments; <=
+    // 256 blocks: the 64-bit sum cannot wrap.)
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const uint32_t x = wave_incl_scan(v);  // 32-bit: used only when the total fits
+    const uint64_t s64 = wave_sum64(v);
+    const bool w_ragged = __ballot(nn != 0u) != 0, w_mixed = __ballot(u != u0) != 0;
+    if (lane == 0) {
+        pl->wsum[wv] = (uint32_t)min(s64, (uint64_t)0xffffffffu);
+        pl->wsum[16u + wv] = (w_ragged ? 1u : 0u) | (w_mixed ? 2u : 0u);
+    }
+    __syncthreads();
+    uint64_t all = 0;
+    uint32_t flags = 0, before = 0;
+    for (uint32_t k = 0; k < nw; ++k) {
+        const uint32_t sk = pl->wsum[k];
+        all += sk;
+        before += k < wv ? sk : 0u;
+        flags |= pl->wsum[16u + k];
+    }
+    if (!(flags & 1u)) {  // every message exactly one segment
         t.total = (uint32_t)a.n;
         t.identity = 1u;
         t.uni = 1u;
         return t;
     }
-    // a block over the limit (k_plan stores ~0 segments), or a sum past it
-    // (<= 256 blocks: the 64-bit sum of the words cannot wrap)
-    uint64_t s64 = v;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        s64 += shfl64(s64, (int)((threadIdx.x & 63u) ^ (uint32_t)o));
-    }
-    if ((threadIdx.x & 63u) == 0) {
-        pl->wsum[threadIdx.x >> 6] = (uint32_t)min(s64, (uint64_t)0xffffffffu);
-    }
-    __syncthreads();
-    uint64_t all = 0;
-    for (uint32_t wv = 0; wv < (blockDim.x >> 6); ++wv) {
-        all += pl->wsum[wv];
-    }
-    const int mismatch = __syncthreads_or(u != u0);
     t.identity = 0u;
-    t.uni = (!mismatch && u0 != 0xffffffffu && u0 != 0u) ? u0 : 0u;
+    t.uni = (!(flags & 2u) && u0 != 0xffffffffu && u0 != 0u) ? u0 : 0u;
     if (all > kSegLimit || (t.uni && (uint64_t)a.n * t.uni > kSegLimit)) {
         t.overflow = 1u;
         t.uni = 0u;
@@ -708,10 +712,9 @@ __device__ PlanTotals plan_reduce(const BatchArgs& a, PlanLds* pl, const PlanWor
         t.total = (uint32_t)a.n * t.uni;
         return t;
     }
-    uint32_t ex;
-    t.total = block_scan(v, &ex, pl->wsum);
+    t.total = (uint32_t)all;
     if (j < nb) {
-        pl->boff[j] = ex;
+        pl->boff[j] = before + x - v;
         pl->bu[j] = u;
     }
     __syncthreads();
@@ -866,6 +869,11 @@ __device__ unsigned long long g_fold_trace[kFoldTraceWaves][8];
 #else
 #define FOLD_STAMP(k)
 #endif
+
+#ifndef BMQCRC_SNAKE
+#define BMQCRC_SNAKE 1  // 0: every round in block order (A/B)
+#endif
+constexpr bool kSnakeRounds = BMQCRC_SNAKE != 0;
 
 // Groups whose speculative first pass skipped a message (a block's list for
 // the second pass; past this many the second pass scans the block's groups).
@@ -1022,16 +1030,21 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     const uint32_t rd_off = (uint32_t)lane * 128u + (((uint32_t)lane >> 1) & 7u) * 16u;
     const uint64_t zero = (uint64_t)(uintptr_t)g_zero_line + 16u * ((uint32_t)lane & 7u);
 
-    // Claim k of this block is group WPB (blockIdx.x + G (k / WPB)) + k % WPB
-    // (G = gridDim.x; >= ngroups: none): the groups round 3's grid-stride
-    // waves of this block took, so one-group-per-wave batches keep their
-    // layout -- a block's first WPB groups are adjacent in memory (mapping
-    // claim k to group blockIdx.x + G k instead cost the headline 1.5-2 %,
-    // profiles/r04/ab/; interleaving single groups for size-class-sorted
-    // maps measured the same as these chunks, profiles/r04/ab/rr/)
+    // Claim k of this block is group WPB (b_r + G r) + k % WPB, r = k / WPB
+    // (G = gridDim.x; >= ngroups: none): chunks of WPB adjacent groups, one
+    // per block and round -- one-group-per-wave batches keep round 3's
+    // layout (mapping claim k to group blockIdx.x + G k instead cost the
+    // headline 1.5-2 %, profiles/r04/ab/).  b_r = blockIdx.x in even rounds
+    // and G - 1 - blockIdx.x in odd ones: in a size-class-sorted map the
+    // chunks' work grows (or shrinks) along the map, so the same block taking
+    // chunk b of every round got the largest chunk of each (the 1/8 Zipf
+    // shard's block means fell with the block index, correlation -0.74,
+    // 475-534 us, profiles/r04/fold_trace/).  gid grows with k.
     const uint32_t nbk = gridDim.x;
     auto gid = [&](uint32_t k) {
-        return (blockIdx.x + nbk * (k / (uint32_t)WPB)) * (uint32_t)WPB + k % (uint32_t)WPB;
+        const uint32_t r = k / (uint32_t)WPB;
+        const uint32_t b = (kSnakeRounds && (r & 1u)) ? nbk - 1u - blockIdx.x : blockIdx.x;
+        return (b + nbk * r) * (uint32_t)WPB + k % (uint32_t)WPB;
     };
     // a claim in two halves: the LDS atomic (lane 0) is issued early and its
     // result read later, so its latency hides behind other LDS work

@@ -505,3 +505,30 @@ def test_group_search_maps_every_segment(seed):
         lanes = [s for s in range(64 * g, min(64 * g + 64, total))]
         got = _find_msg_group(first, n, 64 * g, lanes)
         assert got == [(int(owner[s]), int(kidx[s])) for s in lanes], g
+
+
+def _claim_group(k, b, nbk, wpb, snake=True):
+    """k_fold's claim k of block b (crc32c_kernels.hip, gid): chunks of wpb
+    adjacent groups, one per block and round, blocks reversed in odd rounds."""
+    r = k // wpb
+    bb = nbk - 1 - b if snake and r % 2 else b
+    return (bb + nbk * r) * wpb + k % wpb
+
+
+@pytest.mark.parametrize("ngroups,nbk,wpb", [(1, 256, 8), (2047, 256, 8), (2048, 256, 8),
+                                             (16384, 256, 8), (777, 37, 4), (5000, 512, 4)])
+def test_claims_cover_every_group_once(ngroups, nbk, wpb):
+    """Every group is claimed by exactly one (block, k), and a block's claims
+    grow with k, so its first claim past the batch ends its loop (the main
+    loop and the speculative second pass stop there)."""
+    seen = []
+    for b in range(nbk):
+        prev = -1
+        for k in range(ngroups + 2 * wpb):
+            g = _claim_group(k, b, nbk, wpb)
+            assert g > prev
+            prev = g
+            if g >= ngroups:
+                break
+            seen.append(g)
+    assert sorted(seen) == list(range(ngroups))
