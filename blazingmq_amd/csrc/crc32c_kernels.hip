@@ -1043,7 +1043,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     const uint32_t nbk = gridDim.x;
     auto gid = [&](uint32_t k) {
         const uint32_t r = k / (uint32_t)WPB;
-        const uint32_t b = (kSnakeRounds && (r & 1u)) ? nbk - 1u - blockIdx.x : blockIdx.x;
+        const uint32_t b = (kSnakeRounds && !ONE && (r & 1u)) ? nbk - 1u - blockIdx.x : blockIdx.x;
         return (b + nbk * r) * (uint32_t)WPB + k % (uint32_t)WPB;
     };
     // a claim in two halves: the LDS atomic (lane 0) is issued early and its
@@ -1136,6 +1136,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     auto segments = [&](uint32_t len) {
         return len ? (seg_shift ? ((len - 1u) >> seg_shift) : (len - 1u) / SEG) + 1u : 0u;
     };
+    bool long_seen = false;  // ONE: a message of this wave's groups needs the second pass
     // The segment of group gg in this lane (planned or speculative mapping).
     auto setup = [&](const SegDesc& d, uint32_t gg, Group& G) {
         const uint32_t seg = gg * 64u + (uint32_t)lane;
@@ -1146,7 +1147,9 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
             // the wave's second pass (below); with u = 1 an empty message is
             // folded whole (its seed)
             const bool ok = spec_u == 1u ? nseg <= 1u : nseg == spec_u;
-            if (__ballot(valid && !ok) != 0 && lane == 0) {  // group gg goes on the block's list
+            if constexpr (ONE) {
+                long_seen |= __ballot(valid && !ok) != 0;
+            } else if (__ballot(valid && !ok) != 0 && lane == 0) {  // group gg on the block's list
                 const uint32_t at = atomicAdd(&long_n, 1u);
                 if (at < kLongListCap) {
                     long_list[at] = gg;
@@ -1331,12 +1334,19 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     // block's groups are scanned if it overflowed), shared out over its
     // waves.  No wave waits on another block, and in the predicted case
     // (every message as predicted) no wave runs this pass.
+    //
+    // The speculative one-segment kernel (ONE) runs round 3's form: the wave
+    // flags its own groups (long_seen) and scans them again.  (Sharing the
+    // claiming kernels' block list there, or dropping the pass, changed
+    // ONE's code generation and cost one-line groups 15 %: 64-byte messages
+    // 96 against 82 us, profiles/r04/ab/small_msgs/.)
     auto second_pass = [&](uint32_t nlong) {
         bool any = false;
         const uint32_t mpg = 64u / spec_u;  // messages per group
         const bool listed = nlong <= kLongListCap;
         for (uint32_t j = wave;; j += WPB) {
-            const uint32_t gg = listed ? (j < nlong ? long_list[j] : ngroups) : gid(j);
+            const uint32_t gg = ONE ? gfirst + (j / (uint32_t)WPB) * nbk * (uint32_t)WPB
+                                : listed ? (j < nlong ? long_list[j] : ngroups) : gid(j);
             if (gg >= ngroups) {
                 break;
             }
@@ -1386,10 +1396,72 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     // (descriptors loading), g2 the one after (map entries loading); each
     // new one is claimed from the block's counter, so a wave that runs
     // faster takes more of the block's groups.
-    uint32_t g = gid(wave), g1 = ngroups, g2 = ngroups;  // (= gfirst)
     Group G;
     SegDesc nxt = {0ull, 0u, 0u, 0u, 0u};
     SegRef ref2 = {0u, 0u};
+    if constexpr (ONE) {
+        // The speculative one-segment kernel: every group the same work, so
+        // wave w of block b keeps round 3's static share, groups
+        // g0 + j stride (the set its claims k = w, w + WPB, ... name, gid
+        // without the reversed rounds), in the grid-stride loop of round 3.
+        // (The claiming loop below compiled for ONE ran one-line groups
+        // 15 % slower -- 64-byte messages 95 against 82 us, 128 B 70 against
+        // 64, 256 B 50.7 against 49.5 -- with claims, list and layout each
+        // ruled out, profiles/r04/ab/small_msgs/.)
+        const uint32_t stride = nbk * (uint32_t)WPB;
+        uint32_t g = gfirst;
+        if (g < ngroups) {
+            const uint32_t s0 = g * 64u + (uint32_t)lane;
+            SegRef r0 = {0u, 0u};
+            if (!identity) {
+                r0 = map_segment(a, &pl, s0, s0 < total, identity, uni, sorted, ep);
+                if (sorted) {
+                    r0 = resolve_sorted(r0, s0 < total);
+                }
+            }
+            const SegDesc d0 = identity ? spec : fetch_desc(a, r0, s0 < total);
+            const uint32_t s1 = (g + stride) * 64u + (uint32_t)lane;
+            const bool v1 = g + stride < ngroups && s1 < total;
+            SegRef r1 = map_segment(a, &pl, s1, v1, identity, uni, sorted, ep);
+            if (sorted) {
+                r1 = resolve_sorted(r1, v1);
+            }
+            nxt = fetch_desc(a, r1, v1);
+            const uint32_t s2 = (g + 2u * stride) * 64u + (uint32_t)lane;
+            ref2 = map_segment(a, &pl, s2, g + 2u * stride < ngroups && s2 < total, identity, uni,
+                               sorted, ep);
+            setup(d0, g, G);
+            issue_first_rounds(G);
+            FOLD_STAMP(2)
+        }
+        [[maybe_unused]] bool first = true;
+        for (; g < ngroups; g += stride) {
+            uint32_t Rm[32];
+            fold_rounds(G, Rm);
+#if BMQCRC_FOLD_DIAG
+            if (first) {
+                FOLD_STAMP(3)
+                first = false;
+            }
+            if (g + stride >= ngroups) {
+                FOLD_STAMP(4)
+            }
+#endif
+            const Group C = G;
+            if (g + stride < ngroups) {
+                setup(nxt, g + stride, G);
+                const uint32_t s2 = (g + 2u * stride) * 64u + (uint32_t)lane;
+                const bool v2 = g + 2u * stride < ngroups && s2 < total;
+                nxt = fetch_desc(a, sorted ? resolve_sorted(ref2, v2) : ref2, v2);
+                const uint32_t s3 = (g + 3u * stride) * 64u + (uint32_t)lane;
+                ref2 = map_segment(a, &pl, s3, g + 3u * stride < ngroups && s3 < total, identity,
+                                   uni, sorted, ep);
+                issue_first_rounds(G);
+            }
+            finish(C, C.hskip ? tail_horner<8>(Rm, tab_lds) : tail_horner(Rm, tab_lds));
+        }
+    } else {
+    uint32_t g = gid(wave), g1 = ngroups, g2 = ngroups;  // (= gfirst)
     if (g < ngroups) {
         g1 = claim();
         g2 = g1 < ngroups ? claim() : ngroups;
@@ -1452,8 +1524,13 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
         g1 = g2;
         g2 = g3;
     }
+    }
     FOLD_STAMP(5)
-    if (spec_mode) {
+    if constexpr (ONE) {
+        if (long_seen) {
+            second_pass(0u);
+        }
+    } else if (spec_mode) {
         __syncthreads();  // the block's list of groups with skipped messages is complete
         const uint32_t nlong = long_n;
         if (nlong) {
