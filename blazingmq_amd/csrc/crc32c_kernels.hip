@@ -881,9 +881,10 @@ constexpr uint32_t kLongListCap = 64;
 
 // ONE: a speculative launch predicting one segment per message (spec == 1),
 // compiled apart so the first pass knows k = 0 and nseg = 1 (no planner words,
-// no move to the message end, no run combine).
+// no move to the message end, no run combine); it keeps static grid-stride
+// shares (below).
 // WPB: waves per block.  8 = one block of two waves per SIMD per CU (round
-// 4), whose waves take the block's groups from an LDS counter as they go:
+// 4), whose waves (ONE aside) take the block's groups from an LDS counter:
 // with two 4-wave blocks per CU and a static grid-stride share each, the
 // CU's second block ran its waves 9 % longer (later start, then less issue
 // share) and the launch ended on it (tools/fold_trace_diag.py,
@@ -897,8 +898,9 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     // remainder tables, DMA slots, move factors (not needed by ONE: no moves
     // in its first pass)
     __shared__ __attribute__((aligned(16))) uint8_t lds[kTabBytes + kLds + (ONE ? 0 : kXbBytes)];
-    // group claims: the block owns groups blockIdx.x + k gridDim.x, k = 0, 1,
-    // ...; wave w starts with k = w, later k come from this counter
+    // group claims (gid below): wave w starts with claim k = w, later k come
+    // from this counter; long_n / long_list: the block's groups with a message
+    // its speculative first pass skipped
     __shared__ uint32_t claim_ctr, long_n;
     __shared__ uint32_t long_list[kLongListCap];
 
