@@ -114,7 +114,7 @@ def parse():
     p.add_argument("--no-strong-scaling", action="store_true",
                    help="N > 1: skip the strong-scaled Zipf object")
     p.add_argument("--plan-wait-us", type=int, default=None,
-                   help="bmqcrc_plan_wait limit for this run (default: the library's 1000 us; "
+                   help="bmqcrc_plan_wait limit for this run (default: the library's 100 us; "
                         "0 gives every ragged batch's size-class map up: the fallback's cost)")
     p.add_argument("--launch-check", action="store_true",
                    help="test hook: start the ranks, rendezvous over gloo and print the "
@@ -571,7 +571,7 @@ def main():
         step(False)
     torch.cuda.synchronize(dev)
     bmq.kernel_timing(local, stream)  # reset
-    wait_us = 1000 if args.plan_wait_us is None else args.plan_wait_us
+    wait_us = 100 if args.plan_wait_us is None else args.plan_wait_us
     voided0 = bmq.plan_wait(local, stream, wait_us)  # given-up planner maps so far
 
     if world > 1:

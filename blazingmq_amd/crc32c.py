@@ -346,11 +346,11 @@ def forget_shape(device, stream):
     _native.check(_native.lib.bmqcrc_forget_shape(device, stream.cuda_stream))
 
 
-def plan_wait(device, stream, wait_us=1000):
+def plan_wait(device, stream, wait_us=100):
     """Longest wait (microseconds) of the single-pass planner's blocks for
     each other on (device, stream) before a ragged batch's size-class map is
-    given up (bmqcrc_plan_wait; results stay exact, the fold then takes every
-    message whole in one lane).
+    given up (bmqcrc_plan_wait, default 100; results stay exact, the fold then
+    searches the per-message segment offsets instead of the size-class map).
     Returns how many planned batches there gave up their map so far."""
     n = ctypes.c_uint64()
     _native.check(_native.lib.bmqcrc_plan_wait(device, stream.cuda_stream, int(wait_us),

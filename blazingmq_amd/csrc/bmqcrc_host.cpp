@@ -105,7 +105,7 @@ struct Workspace {
     std::mutex mu;
     DevBuf seg_first, block_sum, seginfo, firstk, gdesc, bhist, plan_sync;
     uint32_t plan_epoch = 0;  // k_plan_map launches on this workspace (BatchArgs::plan_epoch)
-    uint64_t map_wait_ticks = 100000;  // 1 ms (bmqcrc_plan_wait)
+    uint64_t map_wait_ticks = 10000;  // 100 us (bmqcrc_plan_wait)
 
     // host-pointer staging
     DevBuf arena, offsets, lengths, seeds, out;

@@ -204,7 +204,9 @@ int bmqcrc_forget_shape(int device, void* stream);
 
 /* ABI 2.3.  Longest time (microseconds) the blocks of the single-pass
  * planner (ragged batches) wait for each other on (device, stream) before
- * giving up the size-class map of that batch; default 1000.  The planner's
+ * giving up the size-class map of that batch; default 100 (1000 before round
+ * 4's final build: eight processes sharing one GPU then spun up to 1 ms per
+ * planner launch).  The planner's
  * blocks meet once, grid-wide, and its grid never exceeds what the device
  * holds at once; when the GPU still cannot run them all together (other
  * streams or processes hold the CUs) a block that waited this long gives the

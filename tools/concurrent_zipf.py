@@ -37,7 +37,7 @@ def main():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--seg-bytes", type=int, default=0, help="0: automatic")
-    p.add_argument("--wait-us", default="1000",
+    p.add_argument("--wait-us", default="100",
                    help="bmqcrc_plan_wait limits to run the concurrent legs with (comma list)")
     a = p.parse_args()
     dev = torch.device("cuda", 0)
