@@ -106,6 +106,11 @@ def parse():
     p.add_argument("--cpu-table", action="store_true",
                    help="CPU baseline table (DESIGN.md section 6): every config, the three "
                         "bdlde::Crc32c variants restated in oracle/, 1 and up to 16 threads")
+    p.add_argument("--scalar", action="store_true",
+                   help="the drop-in scalar bmqp::Crc32c::calculate (pointer and 4 KiB-buffer "
+                        "Blob forms, tools/bin/scalar_ladder) on the reference's size ladder, "
+                        "beside its published times and the oracle's SSE4.2 3-way and serial "
+                        "crc32q loops; one JSON line per size (no GPU)")
     p.add_argument("--protocol", action="store_true",
                    help="measure the batch callers of SURVEY.md 8(f): partition recovery "
                         "verify, deferred PUT-event CRCs, Blob batches, ledger validation")
@@ -259,6 +264,49 @@ def cpu_table(args):
                     "sample_msgs": n, "sample_MiB": round(nbytes / 2**20, 1), "passes": reps,
                     "host": cpu_model(), "nproc": os.cpu_count(),
                     "machine": platform.machine()}), flush=True)
+
+
+# bmqp_crc32c.h:109-132: the reference's default (SSE4.2) time per call, ns,
+# on its size ladder (bmqp_crc32c.t.cpp:95-118), 64-bit build
+REF_LADDER_NS = {11: 9, 16: 9, 21: 10, 59: 13, 64: 12, 69: 13, 251: 30, 256: 30, 261: 37,
+                 1019: 155, 1024: 45, 1029: 50, 4091: 299, 4096: 176, 4101: 190, 16379: 864,
+                 16384: 724, 16389: 754, 65536: 2858, 262144: 11925, 1048576: 50937,
+                 4194304: 198662, 16777216: 796534, 67108864: 9976933}
+
+
+def scalar(args):
+    """The drop-in scalar CRC (what every unbatched caller links) on the
+    reference's size ladder: tools/bin/scalar_ladder times
+    bmqp::Crc32c::calculate(ptr, len) and calculate(Blob of 4 KiB buffers)
+    with the reference's loop (bmqp_crc32c.t.cpp:1116-1120); beside it the
+    oracle's restatement of the reference's SSE4.2 3-way CRC and a serial
+    crc32q chain, the same loop in C, and the published time."""
+    import subprocess
+
+    import numpy as np
+    import oracle
+    exe = os.path.join(ROOT, "tools", "bin", "scalar_ladder")
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=600, check=True).stdout
+    rng = np.random.default_rng(0)
+    buf = rng.integers(0, 256, size=64 << 20, dtype=np.uint8)
+    host = {"host": cpu_model(), "nproc": os.cpu_count(), "threads": 1}
+    for line in out.splitlines():
+        rec = json.loads(line)
+        size = rec["size"]
+        sub = buf[:size]
+        iters = max(20, min(100000, rec["iters"]))
+        t_hw = oracle.time_repeat(sub, iters, "hw")
+        t_ser = oracle.time_repeat(sub, iters, "hw_serial")
+        rec.update({"published_ns": REF_LADDER_NS.get(size),
+                    "published_at": "bmqp_crc32c.h:109-132",
+                    "oracle_3way_ns": round(1e9 * t_hw / iters, 1),
+                    "oracle_serial_crc32q_ns": round(1e9 * t_ser / iters, 1),
+                    "oracle_iters": iters, **host})
+        rec["calculate_over_serial"] = round(rec["calculate_ns"] / rec["oracle_serial_crc32q_ns"], 3)
+        rec["calculate_over_published"] = (round(rec["calculate_ns"] / rec["published_ns"], 3)
+                                           if rec["published_ns"] else None)
+        print(json.dumps(rec), flush=True)
+    return 0
 
 
 def _wall(fn, reps):
@@ -491,6 +539,8 @@ def main():
     args = parse()
     if args.cpu_table:
         return cpu_table(args)
+    if args.scalar:
+        return scalar(args)
     world_env = os.environ.get("WORLD_SIZE")
     if world_env is None and args.gpus > 1:
         return spawn_ranks(args)

@@ -597,6 +597,13 @@ int parse_opts(const bmqcrc_opts* opts, bmqcrc_opts* o, uint32_t* seg, int* dev)
         // it may be built against any earlier, shorter layout
         const size_t given = opts->struct_size ? opts->struct_size : offsetof(bmqcrc_opts, ndevices);
         memcpy(o, opts, std::min<size_t>(sizeof(*o), given));
+        // ABI 2.1-2.4 read the whole struct when struct_size was 0: a caller
+        // of those minors that zero-initialised it, set a later field and
+        // never set struct_size would now lose that field silently -- refuse
+        if (!opts->struct_size && (opts->ndevices || opts->max_len || opts->min_len)) {
+            return fail(BMQCRC_EINVAL, "bmqcrc_opts.struct_size is 0 but a field past ABI 2.0 "
+                                       "(ndevices, max_len, min_len) is set: set struct_size");
+        }
         o->struct_size = sizeof(*o);
     }
     *seg = o->seg_bytes;
@@ -671,25 +678,7 @@ extern "C" void bmqcrc_clear_error(void)
 
 extern "C" {
 
-uint32_t bmqcrc_crc32c(const void* data, uint32_t length, uint32_t crc)
-{
-    return bmqcrc::cpu_crc32c(data, length, crc);
-}
-
-uint32_t bmqcrc_crc32c_blob(const void* const* bufs, const uint32_t* lens, uint32_t nbuf,
-                            uint32_t crc)
-{
-    // bmqp_crc32c.cpp:47-67: an empty blob returns crc; otherwise chain.
-    for (uint32_t i = 0; i < nbuf; ++i) {
-        crc = bmqcrc::cpu_crc32c(bufs[i], lens[i], crc);
-    }
-    return crc;
-}
-
-uint32_t bmqcrc_combine(uint32_t crcA, uint32_t crcB, uint64_t lenB)
-{
-    return bmqcrc::cpu_combine(crcA, crcB, lenB);
-}
+// bmqcrc_crc32c, bmqcrc_crc32c_blob and bmqcrc_combine: crc32c_cpu.cpp
 
 int bmqcrc_crc32c_batch(const void* arena, uint64_t arena_bytes, const uint64_t* offsets,
                         const uint32_t* lengths, const uint32_t* seeds, uint32_t* out,

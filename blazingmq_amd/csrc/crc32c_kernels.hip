@@ -2761,7 +2761,12 @@ extern "C" int bmqcrc_launch_batch(const BatchArgs* a, void* stream, int num_cus
     if (a->n == 0) {
         return 0;
     }
-    if (!a->whole && !a->spec && a->map_planned && single_pass_planner(*a) && a->plan_epoch == 0) {
+    if (!a->whole && !a->spec && a->map_planned && a->plan_epoch == 0) {
+        // whichever planner runs: k_fold's sorted path takes a gdesc word in
+        // place of seginfo when its tag equals the launch's, so a captured
+        // pair-planned batch needs a tag no earlier word carries too (left at
+        // plan_sync[1] it could be 0 -- every zeroed word -- or the tag of an
+        // earlier captured k_plan_map whose words name stale messages)
         hipLaunchKernelGGL(k_epoch_advance, dim3(1), dim3(1), 0, s, a->plan_sync);
     }
     if (!a->whole && !a->spec) {

@@ -28,7 +28,7 @@
  *   oracle_crc32c_bitwise    bit-at-a-time definition (ground truth)
  *   oracle_crc32c_sw         slicing-by-8 tables  (Crc32c_Impl::calculateSoftware)
  *   oracle_crc32c_hw_serial  SSE4.2 crc32q serial (Crc32c_Impl::calculateHardwareSerial)
- *   oracle_crc32c_hw         SSE4.2 3-way interleaved + GF(2) shift-combine
+ *   oracle_crc32c_hw         SSE4.2 3-way interleaved + table shift-combine
  *                            (bdlde::Crc32c::calculate default)
  * Parity of all variants is pinned by tests/golden/ (the reference's golden
  * vectors) in tests/test_oracle_golden.py.
@@ -194,16 +194,29 @@ __attribute__((target("sse4.2"))) static uint32_t hw_raw(const uint8_t *p, size_
 /* Three independent crc32q chains over consecutive thirds of a block, then a
  * GF(2) shift-combine: the standard way to fill the 3-cycle-latency /
  * 1-per-cycle-throughput crc32 pipeline.  Two block tiers (8 KiB, 256 B) so
- * mid-size buffers also run interleaved. */
-static uint32_t g_shift[2][2]; /* [tier][0]=x^(8*2*blk), [tier][1]=x^(8*blk) */
+ * mid-size buffers also run interleaved.  The combine shifts a register over
+ * a lane of zero bytes with four 256-entry tables per tier (one lookup per
+ * register byte), as in the published SSE4.2 CRC-32C code this family of
+ * implementations follows (Mark Adler's crc32c.c: LONG = 8192, SHORT = 256,
+ * crc32c_zeros / crc32c_shift); BDE's own source is absent (header comment). */
+static uint32_t g_zeros[2][4][256]; /* [tier][register byte][value]: shift over one lane */
 static const uint32_t g_blk[2] = {8192u, 256u};
 static pthread_once_t g_shift_once = PTHREAD_ONCE_INIT;
 static void init_shift(void)
 {
     for (int t = 0; t < 2; ++t) {
-        g_shift[t][0] = x8nmodp(2 * (uint64_t)g_blk[t]);
-        g_shift[t][1] = x8nmodp(g_blk[t]);
+        const uint32_t op = x8nmodp(g_blk[t]);
+        for (int k = 0; k < 4; ++k) {
+            for (uint32_t n = 0; n < 256; ++n) {
+                g_zeros[t][k][n] = multmodp(op, n << (8 * k));
+            }
+        }
     }
+}
+
+static inline uint32_t zeros_shift(const uint32_t (*z)[256], uint32_t c)
+{
+    return z[0][c & 0xff] ^ z[1][(c >> 8) & 0xff] ^ z[2][(c >> 16) & 0xff] ^ z[3][c >> 24];
 }
 
 __attribute__((target("sse4.2"))) static uint32_t hw3_raw(const uint8_t *p, size_t len, uint32_t c)
@@ -226,8 +239,8 @@ __attribute__((target("sse4.2"))) static uint32_t hw3_raw(const uint8_t *p, size
                 c1 = _mm_crc32_u64(c1, w1);
                 c2 = _mm_crc32_u64(c2, w2);
             }
-            c = multmodp(g_shift[t][0], (uint32_t)c0) ^ multmodp(g_shift[t][1], (uint32_t)c1) ^
-                (uint32_t)c2;
+            c = zeros_shift(g_zeros[t], (uint32_t)c0) ^ (uint32_t)c1;
+            c = zeros_shift(g_zeros[t], c) ^ (uint32_t)c2;
             p += 3 * (size_t)blk;
             len -= 3 * (size_t)blk;
         }

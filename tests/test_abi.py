@@ -61,6 +61,25 @@ def test_version_and_error_string():
     assert isinstance(lib.bmqcrc_last_error(), bytes)
 
 
+def test_zero_struct_size_with_later_fields_is_refused():
+    # struct_size 0 reads the ABI 2.0 fields only; a caller that also set a
+    # later field (as ABI 2.1-2.4 read them) gets EINVAL, not a silent drop.
+    # The check precedes any device lookup, so it runs without a GPU.
+    from blazingmq_amd import _native as N
+    buf = (ctypes.c_uint8 * 64)()
+    offs = (ctypes.c_uint64 * 1)(0)
+    lens = (ctypes.c_uint32 * 1)(8)
+    out = (ctypes.c_uint32 * 1)()
+    for field in ("ndevices", "max_len", "min_len"):
+        o = N.make_opts(**{field: 2} if field != "ndevices" else {})
+        if field == "ndevices":
+            o.ndevices = 2
+        o.struct_size = 0
+        rc = N.lib.bmqcrc_crc32c_batch(buf, 64, offs, lens, None, out, 1, ctypes.byref(o))
+        assert rc == N.BMQCRC_EINVAL, (field, rc)
+        assert b"struct_size" in N.lib.bmqcrc_last_error()
+
+
 def test_opts_layout_matches_the_header(tmp_path):
     # bmqcrc_opts as the C compiler lays it out (ABI 2.4 appends max_len, 2.5 min_len) and
     # as the ctypes binding does: same size, same field offsets

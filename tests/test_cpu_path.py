@@ -32,7 +32,12 @@ def test_scalar_chained(golden):
 def test_scalar_misaligned_random():
     rng = np.random.default_rng(21)
     big = rng.integers(0, 256, size=300000, dtype=np.uint8)
-    for n in list(range(0, 40)) + [191, 192, 193, 1535, 1536, 1537, 12287, 12288, 12289, 100000]:
+    # the product's method boundaries (crc32c_cpu.cpp): serial below 192 B,
+    # one-accumulator fold below 256, four accumulators, 16-byte and < 16-byte
+    # tails; three-way lanes (hosts without AVX-512) are checked below
+    for n in list(range(0, 40)) + [63, 64, 65, 191, 192, 193, 207, 208, 255, 256, 257, 271, 319,
+                                   320, 511, 512, 513, 767, 1535, 1536, 1537, 12287, 12288, 12289,
+                                   100000, 262147]:
         for mis in range(0, 8):
             buf = big[mis:mis + n]
             seed = int(rng.integers(0, 2**32))
@@ -65,6 +70,28 @@ def test_last_data_buffer_length():
     b = Blob([b"one", b"two", b"threeXYZ"])
     b.set_last_data_buffer_length(5)
     assert Crc32c.calculate_blob(b) == 0xA0EA6901
+
+
+def test_scalar_methods_agree(tmp_path):
+    # every method of crc32c_cpu.cpp the host supports (serial crc32q, the
+    # three-way lanes, the VPCLMULQDQ fold, slicing-by-8) against the bitwise
+    # definition on 20,000 random lengths, seeds and misalignments, plus
+    # combine; built from the same source with the A/B harness
+    exe = tmp_path / "scalar_ab"
+    subprocess.run(["g++", "-O2", "-std=c++17", os.path.join(ROOT, "tools", "scalar_ab.cpp"),
+                    "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe), "check"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and '"bad": 0' in r.stdout, r.stdout + r.stderr
+
+
+def test_combine_long_lengths():
+    # bmqcrc_combine over lengths past 32 bits (every bit of lenB a clmul
+    # step) against the oracle's bit-serial combine
+    rng = np.random.default_rng(43)
+    for _ in range(200):
+        a, b = (int(x) for x in rng.integers(0, 2**32, size=2))
+        lb = int(rng.integers(0, 2**60))  # the oracle forms 8 * lenB in 64 bits
+        assert Crc32c.combine(a, b, lb) == oracle.combine(a, b, lb)
 
 
 def test_combine():

@@ -419,7 +419,7 @@ def test_shape_hint_misprediction(cuda):
         run(lens)
 
 
-def test_planner_map_given_up(cuda):
+def test_planner_map_given_up(cuda, record_property):
     # Ragged batches are planned by one kernel whose blocks meet once,
     # grid-wide.  When they cannot all run at once a block stops waiting after
     # bmqcrc_plan_wait's limit and the map is given up; every block still
@@ -453,16 +453,20 @@ def test_planner_map_given_up(cuda):
     d_seeds = torch.from_numpy(seeds.view(np.int32)).to(cuda)
 
     def run(reps=1):
-        torch.cuda.synchronize(cuda)
-        t0 = time.perf_counter()
+        # the fastest of `reps` synchronised batches: a noisy neighbour on the
+        # GPU or host can only lengthen a sample, so the minimum is the stable
+        # statistic for the ratio asserted below
+        best = float("inf")
         for _ in range(reps):
+            torch.cuda.synchronize(cuda)
+            t0 = time.perf_counter()
             got = Crc32c.calculate_batch(arena, d_offs, d_lens, d_seeds, stream=s,
                                          seg_bytes=2048, sync=False)
-        s.synchronize()
-        dt = (time.perf_counter() - t0) / reps
-        bad = np.nonzero(got.cpu().numpy().view(np.uint32) != exp)[0]
-        assert bad.size == 0, [(int(i), int(lens[i])) for i in bad[:8]]
-        return dt
+            s.synchronize()
+            best = min(best, time.perf_counter() - t0)
+            bad = np.nonzero(got.cpu().numpy().view(np.uint32) != exp)[0]
+            assert bad.size == 0, [(int(i), int(lens[i])) for i in bad[:8]]
+        return best
 
     v0 = plan_wait(cuda.index, s)
     run()
@@ -474,7 +478,11 @@ def test_planner_map_given_up(cuda):
     v1 = plan_wait(cuda.index, s, 1000)
     assert v1 == v0 + 6  # the zero limit gives up every launch's map
     print("mapped %.3f ms, given up %.3f ms per batch" % (1e3 * t_map, 1e3 * t_void))
-    assert t_void < 2.0 * t_map + 1e-3, (t_map, t_void)
+    record_property("given_up_over_mapped", round(t_void / t_map, 3))
+    # DESIGN.md 4 claims 1.14x on Zipf; the wall clock here includes the
+    # launch and synchronisation overhead common to both, so the margin is
+    # 1.3x plus 0.2 ms
+    assert t_void < 1.3 * t_map + 2e-4, (t_map, t_void)
     run()  # back to mapping
     assert plan_wait(cuda.index, s) == v1
 

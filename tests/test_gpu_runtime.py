@@ -101,6 +101,60 @@ def test_graph_replays_of_a_ragged_batch_with_new_lengths(cuda):
         assert bad.size == 0, (it, bad[:8])
 
 
+def test_graph_capture_while_the_pair_plans(cuda):
+    # A given-up map switches the workspace to the pair planner (k_plan +
+    # k_plan_sort) for its next ragged batches.  A batch captured then carries
+    # device-side tags (plan_epoch 0) as in the single-pass case: k_fold's
+    # group-descriptor lookup must not match words left at tag 0 (never
+    # written) or by an earlier launch, so every replay must stay exact.
+    import torch
+    from blazingmq_amd import last_launch, plan_wait
+    rng = np.random.default_rng(37)
+    size, n = 16 << 20, 1_400_100
+    side = torch.cuda.Stream(cuda)
+    arena = torch.zeros(size, dtype=torch.uint8, device=cuda)
+    o = torch.zeros(n, dtype=torch.int64, device=cuda)
+    ln = torch.zeros(n, dtype=torch.int32, device=cuda)
+    out = torch.zeros(n, dtype=torch.int32, device=cuda)
+    reserve(cuda.index or 0, side, n, size, 2048)
+
+    def new_batch():
+        lens = np.concatenate([rng.integers(0, 300, size=n - 100),
+                               rng.integers(0, 100000, size=100)]).astype(np.uint32)
+        rng.shuffle(lens)
+        offs = (rng.random(n) * (size - lens + 1)).astype(np.int64)
+        data = rng.integers(0, 256, size=size, dtype=np.uint8)
+        arena.copy_(torch.from_numpy(data).to(cuda))
+        o.copy_(torch.from_numpy(offs).to(cuda))
+        ln.copy_(torch.from_numpy(lens.view(np.int32)).to(cuda))
+        torch.cuda.synchronize()
+        return oracle.batch(data, offs, lens, None, nthreads=8)
+
+    def run():
+        with torch.cuda.stream(side):
+            Crc32c.calculate_batch(arena, o, ln, None, out, stream=side, sync=False,
+                                   seg_bytes=2048)
+        side.synchronize()
+
+    exp = new_batch()
+    run()  # warm: ragged, mapped by the single pass
+    plan_wait(cuda.index or 0, side, 0)
+    run()  # the zero limit gives the map up (recorded on the workspace)
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), exp)
+    plan_wait(cuda.index or 0, side, 1000)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        Crc32c.calculate_batch(arena, o, ln, None, out, stream=side, sync=False, seg_bytes=2048)
+    assert last_launch(cuda.index or 0, side)["kernels"] == 3  # k_plan + k_plan_sort + k_fold
+    for it in range(4):
+        exp = new_batch()
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        bad = np.nonzero(out.cpu().numpy().view(np.uint32) != exp)[0]
+        assert bad.size == 0, (it, bad[:8])
+
+
 def test_concurrent_streams_and_threads(cuda):
     import torch
     rng = np.random.default_rng(41)
