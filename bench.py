@@ -118,6 +118,12 @@ def parse():
                    help="end-to-end mode: H2D from pinned host + CRC + D2H (for DESIGN.md)")
     p.add_argument("--no-strong-scaling", action="store_true",
                    help="N > 1: skip the strong-scaled Zipf object")
+    p.add_argument("--rotate", type=int, default=1,
+                   help="N > 1: every step (settle, warmup, timed, planned, declared, kernel "
+                        "timing) takes the next of N copies of the batch (arena, offsets, "
+                        "lengths, out), so a batch smaller than the 256 MiB Infinity Cache is "
+                        "read from HBM rather than replayed from the cache (configs[1]: "
+                        "--rotate 4 cycles 1.1 GiB)")
     p.add_argument("--plan-wait-us", type=int, default=None,
                    help="bmqcrc_plan_wait limit for this run (default: the library's 100 us; "
                         "0 gives every ragged batch's size-class map up: the fallback's cost)")
@@ -594,23 +600,32 @@ def main():
     total_bytes = int(lens_np.sum(dtype=np.uint64))
     # This rank's messages are bytes [begin, begin + total) of synthetic stream
     # `seed`, generated in HBM; offsets are relative to the rank's arena.
-    arena = torch.empty(max(total_bytes, 8), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
-    _fill_slice(bmq, arena, seed, begin)
-    offsets = torch.from_numpy(offs_np).to(dev)
-    lengths = torch.from_numpy(lens_np.view(np.int32)).to(dev)
-    out = torch.empty(n, dtype=torch.int32, device=dev)
+    rotate = max(1, args.rotate)
+    copies = []  # --rotate: N independent copies of the batch, one per step in turn
+    for _ in range(rotate):
+        arena = torch.empty(max(total_bytes, 8), dtype=torch.uint8, device=dev)
+        _fill_slice(bmq, arena, seed, begin)
+        copies.append((arena, torch.from_numpy(offs_np).to(dev),
+                       torch.from_numpy(lens_np.view(np.int32)).to(dev),
+                       torch.empty(n, dtype=torch.int32, device=dev)))
+    arena, offsets, lengths, out = copies[0]
     torch.cuda.synchronize(dev)
 
     if args.e2e:
         return e2e(args, dev, stream, arena, offs_np, lens_np, total_bytes, world, rank, dist,
                    desc)
 
+    turn = [0]
+
     def step(timed, plan=False, max_len=0, min_len=0):
-        Crc32c.calculate_batch(arena, offsets, lengths, None, out, seg_bytes=args.seg_bytes,
-                               stream=stream, sync=False, time_kernel=timed,
-                               whole_messages=args.whole_messages, plan=plan, max_len=max_len,
-                               min_len=min_len)
+        nonlocal out
+        arena_i, offsets_i, lengths_i, out = copies[turn[0] % rotate]
+        turn[0] += 1
+        Crc32c.calculate_batch(arena_i, offsets_i, lengths_i, None, out,
+                               seg_bytes=args.seg_bytes, stream=stream, sync=False,
+                               time_kernel=timed, whole_messages=args.whole_messages, plan=plan,
+                               max_len=max_len, min_len=min_len)
 
     # setup: settle the GPU clocks under this exact load (not part of W or K)
     t_settle = time.perf_counter()
@@ -676,7 +691,7 @@ def main():
             step(True)
         torch.cuda.synchronize(dev)
     kern_ms, kern_cnt = bmq.kernel_timing(local, stream)
-    del arena  # the strong-scaling leg below needs the memory
+    del arena, copies  # the strong-scaling leg below needs the memory
     bytes_all = total_bytes
     kern_max = kern_ms / max(kern_cnt, 1)
     plan_voided = [voided1 - voided0, voided2 - voided1]
@@ -737,7 +752,10 @@ def main():
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic (splitmix64 random payload bytes generated in HBM)",
-            "config": {"workload": args.config + ": " + desc,
+            "config": {"workload": args.config + ": " + desc
+                       + ("; steps rotate over %d copies of the batch (%.0f MiB, past the "
+                          "256 MiB Infinity Cache)" % (rotate, rotate * (total_bytes + 16 * n)
+                                                       / 2**20) if rotate > 1 else ""),
                        "n_msgs_total": n_all, "payload_bytes_total": bytes_all,
                        "seg_bytes": args.seg_bytes or "auto",
                        "whole_messages": bool(args.whole_messages),

@@ -39,7 +39,8 @@ namespace {
 
 constexpr uint32_t kPoly = 0x82F63B78u;  // 0x1EDC6F41 reflected
 constexpr uint32_t kOne = 1u << 31;      // x^0
-constexpr uint32_t kFoldMin = 192;       // bytes, with AVX-512 VPCLMULQDQ; measured
+constexpr uint32_t kFoldMin = 256;       // bytes, with AVX-512 VPCLMULQDQ (EPYC 9575F: serial
+                                         // crc32q is faster to 224 B, profiles/r05/scalar)
 constexpr uint32_t kThreeWayMin = 256;   // bytes, without it ("Scalar CRC")
 constexpr uint32_t kMaxLane = 4096;      // longest 3-way lane (bytes): 12 KiB per stitch
 

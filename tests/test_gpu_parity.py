@@ -676,6 +676,59 @@ def test_speculative_single_launch(cuda):
         run(lens, tag)
 
 
+@pytest.mark.parametrize("n", [1_000, 100_003, 600_000])
+def test_one_segment_pipeline_shapes(cuda, n):
+    """The one-segment kernel's rolling pipeline (round 5): a slot is
+    refilled with the next round of the wave's stream of groups -- the same
+    group's next line or the next group's first lines -- so consecutive
+    groups of different line counts (1 to 17 lines at 2 KiB segments) follow
+    each other in the slots, with descriptors loaded ahead by LDS-DMA (full
+    groups) or directly (the partial last group).  Declared bounds make every
+    batch ONE launch; 4-wave blocks (n = 1,000 and 100,003) and 8-wave
+    blocks (600,000); with and without seeds; blocks of one line count
+    alternate with mixed ones; a few messages past the bound go to the
+    second pass."""
+    import torch
+    from blazingmq_amd.crc32c import last_launch
+    rng = np.random.default_rng(94 + n)
+    arena_np = rng.integers(0, 256, size=80 << 20, dtype=np.uint8)
+    arena = torch.from_numpy(arena_np).to(cuda)
+    s = torch.cuda.Stream(cuda)
+
+    def run(lens, tag, seeds=True, aligned=False):
+        lens = np.asarray(lens, np.uint32)
+        if aligned:  # contiguous, like the bench (every stream starts on a line)
+            offs = np.zeros(lens.size, np.int64)
+            np.cumsum(lens[:-1], out=offs[1:])
+        else:
+            offs = np.array(rng.integers(0, arena_np.size - lens.astype(np.int64) + 1), np.int64)
+        sd = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64).astype(np.uint32)
+        got = Crc32c.calculate_batch(arena, torch.from_numpy(offs).to(cuda),
+                                     torch.from_numpy(lens.view(np.int32)).to(cuda),
+                                     torch.from_numpy(sd.view(np.int32)).to(cuda) if seeds else None,
+                                     stream=s, seg_bytes=2048, max_len=2048)
+        s.synchronize()
+        exp = oracle.batch(arena_np, offs, lens, sd if seeds else None, nthreads=8)
+        bad = np.nonzero(got.cpu().numpy().view(np.uint32) != exp)[0]
+        assert bad.size == 0, (tag, [(int(i), int(lens[i])) for i in bad[:8]])
+        ll = last_launch(cuda.index, s)
+        assert ll["kernels"] == 1 and ll["spec"] == 1, (tag, ll)
+
+    per_group = rng.choice([1, 60, 128, 256, 500, 2048], size=(n + 63) // 64)
+    blocky = np.repeat(per_group, 64)[:n]       # one line count per group, varying
+    mixed = rng.integers(0, 2049, size=n)
+    run(mixed, "mixed")
+    run(mixed, "mixed, no seeds", seeds=False)
+    run(blocky, "one length per group")
+    run(np.where(rng.integers(0, 2, size=n) == 0, blocky, mixed), "half and half", seeds=False)
+    run(np.full(n, 256), "256 B contiguous", aligned=True, seeds=False)
+    run(np.full(n, 64), "64 B contiguous", aligned=True)
+    run(rng.integers(0, 129, size=n), "one line or two")
+    past = rng.integers(0, 2049, size=n)
+    past[rng.integers(0, n, size=max(1, n // 20000))] = rng.integers(2049, 100_000)
+    run(past, "a few past the bound")
+
+
 def test_declared_max_len_single_launch(cuda):
     """bmqcrc_opts.max_len (ABI 2.4): a device-resident batch whose declared
     bound fits one segment is ONE k_fold launch even right after a ragged
