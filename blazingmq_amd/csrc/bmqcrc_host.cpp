@@ -461,7 +461,14 @@ int run_batch(Ctx& c, uint32_t flags, uint32_t seg, const void* arena, uint64_t 
             a.spec = hint_u;
         }
     }
-    if (!a.whole && host_max_len <= a.seg_bytes && !(flags & BMQCRC_F_PLAN)) {
+    if ((kTuneBits & 2048u) && !a.whole && (flags & BMQCRC_F_PLAN) &&
+        spec_eligible(c, n, a.blocks_per_cu)) {
+        // A/B only (TUNE bit 11): a batch with no shape history launched as
+        // the speculative one-segment kernel instead of being planned (its
+        // second pass folds the longer messages); bench.py's planned leg
+        // then prices that choice
+        a.spec = 1;
+    } else if (!a.whole && host_max_len <= a.seg_bytes && !(flags & BMQCRC_F_PLAN)) {
         a.spec = 1;  // known, not guessed: every message is one segment
     } else if (!a.whole && host_min_len > 0 && host_max_len != UINT64_MAX &&
                !(flags & BMQCRC_F_PLAN)) {

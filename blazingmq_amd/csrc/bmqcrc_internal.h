@@ -29,7 +29,9 @@ constexpr int kBuckets = 16;            // segment size classes: floor(log2(line
 // batches with the round-2 pair k_plan<true> + k_plan_sort instead of the
 // single-pass k_plan_map, bit9 gives planner blocks whole tiles, bit10 keeps
 // two 4-wave k_fold blocks per CU with static group shares (round 3's schedule)
-// instead of one 8-wave block claiming groups dynamically (A/B).
+// instead of one 8-wave block claiming groups dynamically (A/B), bit11
+// launches BMQCRC_F_PLAN batches as the speculative one-segment kernel instead
+// of planning them (the cost of speculating on a stream with no history).
 #ifndef BMQCRC_TUNE_BITS
 #define BMQCRC_TUNE_BITS 0u
 #endif

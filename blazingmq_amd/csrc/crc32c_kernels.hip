@@ -873,48 +873,6 @@ __device__ unsigned long long g_fold_trace[kFoldTraceWaves][8];
 #ifndef BMQCRC_SNAKE
 #define BMQCRC_SNAKE 1  // 0: every round in block order (A/B)
 #endif
-#ifndef BMQCRC_ONE_ROLLING
-#define BMQCRC_ONE_ROLLING 1  // 0: round 4's group-at-a-time ONE loop (A/B)
-#endif
-constexpr bool kOneRolling = BMQCRC_ONE_ROLLING != 0;
-
-// s_waitcnt vmcnt(n) for a wave-uniform n known only at run time: every
-// vector memory load of the rolling ONE loop is this wave's own asm (LDS-DMA),
-// counted in issue order, so "round X has landed" is "at most the loads issued
-// after it are outstanding".  Loads return in order; stores (which may not)
-// are left out of the count, which can only make a wait longer.  n above the
-// largest case waits for more than needed, never for less.
-__device__ __forceinline__ void wait_vm(uint32_t n)
-{
-    switch (n) {
-#define BMQCRC_VM(k)                                               \
-    case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); \
-        return;
-        BMQCRC_VM(0) BMQCRC_VM(1) BMQCRC_VM(2) BMQCRC_VM(3) BMQCRC_VM(4) BMQCRC_VM(5)
-        BMQCRC_VM(6) BMQCRC_VM(7) BMQCRC_VM(8) BMQCRC_VM(9) BMQCRC_VM(10) BMQCRC_VM(11)
-        BMQCRC_VM(12) BMQCRC_VM(13) BMQCRC_VM(14) BMQCRC_VM(15) BMQCRC_VM(16) BMQCRC_VM(17)
-        BMQCRC_VM(18)
-#undef BMQCRC_VM
-    default: asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
-    }
-}
-
-// One LDS-DMA load of a full group's descriptors (1 KiB): lanes 0-31 its 64
-// offsets, 32-47 its 64 lengths, 48-63 its 64 seeds (the zero line when the
-// batch has none), 16 bytes per lane at M0 + 16 * lane.
-__device__ __forceinline__ void desc_dma(uint32_t lds_dst, uint64_t src)
-{
-    uint32_t keep;
-    asm volatile("s_waitcnt lgkmcnt(0)\n\t"
-                 "s_mov_b32 %0, m0\n\t"
-                 "s_mov_b32 m0, %1\n\t"
-                 "s_nop 0\n\t"
-                 "global_load_lds_dwordx4 %2, off\n\t"
-                 "s_mov_b32 m0, %0\n\t"
-                 : "=&s"(keep)
-                 : "s"(lds_dst), "v"(src)
-                 : "memory", "scc");
-}
 constexpr bool kSnakeRounds = BMQCRC_SNAKE != 0;
 
 // Groups whose speculative first pass skipped a message (a block's list for
@@ -937,13 +895,9 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
 {
     constexpr uint32_t kThreads = WPB * 64;
     constexpr int kLds = WPB * kSlots * kSlotBytes;
-    // rolling ONE loop: descriptor buffers per wave (1 KiB each; two with
-    // 8-wave blocks, one with two 4-wave blocks per CU, which must fit 160 KiB)
-    constexpr uint32_t kDescBufs = WPB == 8 ? 2u : 1u;
-    constexpr int kDescLds = (ONE && kOneRolling) ? WPB * (int)kDescBufs * 1024 : 0;
     // remainder tables, DMA slots, move factors (not needed by ONE: no moves
-    // in its first pass) or ONE's descriptor buffers
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kTabBytes + kLds + (ONE ? kDescLds : kXbBytes)];
+    // in its first pass)
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kTabBytes + kLds + (ONE ? 0 : kXbBytes)];
     // group claims (gid below): wave w starts with claim k = w, later k come
     // from this counter; long_n / long_list: the block's groups with a message
     // its speculative first pass skipped
@@ -1447,246 +1401,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     Group G;
     SegDesc nxt = {0ull, 0u, 0u, 0u, 0u};
     SegRef ref2 = {0u, 0u};
-    if constexpr (ONE && kOneRolling) {
-        // Rolling two-slot pipeline (round 5).  The wave's rounds are issued
-        // and folded as one stream across its groups: a slot is refilled with
-        // the next round of that stream -- its group's round r + 2, or the
-        // next group's first rounds -- as soon as its line is in registers,
-        // so both slots stay in flight while a group is folded and while its
-        // remainder is reduced and stored.  (Round 4 issued a group's rounds
-        // only after the previous group's last line: the slots sat idle from
-        // there until the next group was set up.)  The next group is set up
-        // before the wait that precedes its first refill, from descriptors
-        // LDS-DMA'd kDescBufs groups ahead: a compiler-visible load there
-        // would make the compiler's own wait for it drain the data rounds,
-        // whose asm loads it cannot see.
-        const uint32_t stride = nbk * (uint32_t)WPB;
-        const uint32_t desc_lds = tab_lds + kTabBytes + kLds + wave * (kDescBufs * 1024u);
-        struct Fld {  // what the fold and the store of one group need, per lane
-            uint32_t msg, padE, r0, sl, jE, eE, c0;
-            bool valid, lo_part, hi_part;
-            uint32_t R, hskip;  // wave-uniform
-        };
-        // the producer: ordinal p_j (group gfirst + p_j * stride) has p_R
-        // rounds, p_r of them issued; pseq / cseq count the rounds issued /
-        // folded (slot = count & 1); issued counts this wave's DMA loads, and
-        // *_end the count right after each slot's or buffer's load
-        uint64_t pbase[8];
-        uint32_t plo[8], pcnt[8];
-        uint32_t p_j = 0, p_R = 0, p_r = 0, pseq = 0, cseq = 0, nq = 0;
-        uint32_t issued = 0, slot_end0 = 0, slot_end1 = 0, desc_end0 = 0, desc_end1 = 0;
-        Fld F0, F1, F2;  // the group being folded and up to two set up ahead (nq)
-        auto group_of = [&](uint32_t j) { return gfirst + j * stride; };
-        auto full_group = [&](uint32_t gg) { return (uint64_t)gg * 64u + 64u <= a.n; };
-        // descriptors of ordinal j (>= 1) into buffer (j - 1) % kDescBufs; the
-        // batch's last, partial group reads its own (fetch_desc, once a wave)
-        auto desc_issue = [&](uint32_t j) __attribute__((always_inline)) {
-            const uint32_t gg = group_of(j);
-            if (gg >= ngroups || !full_group(gg)) {
-                return;
-            }
-            const uint32_t b = (j - 1u) % kDescBufs;
-            const uint64_t m0 = (uint64_t)gg * 64u;
-            const uint32_t l = (uint32_t)lane;
-            uint64_t src;
-            if (l < 32u) {
-                src = (uint64_t)(uintptr_t)(a.offsets + m0) + 16u * l;
-            } else if (l < 48u) {
-                src = (uint64_t)(uintptr_t)(a.lengths + m0) + 16u * (l - 32u);
-            } else {
-                src = a.seeds ? (uint64_t)(uintptr_t)(a.seeds + m0) + 16u * (l - 48u) : zero;
-            }
-            desc_dma(desc_lds + b * 1024u, src);
-            issued += 1u;
-            if (b == 0u) {
-                desc_end0 = issued;
-            } else {
-                desc_end1 = issued;
-            }
-        };
-        auto desc_read = [&](uint32_t j) __attribute__((always_inline)) {
-            const uint32_t gg = group_of(j);
-            const uint32_t sid = gg * 64u + (uint32_t)lane;
-            if (!full_group(gg)) {
-                return fetch_desc(a, SegRef{sid, 0u}, sid < total);
-            }
-            const uint32_t b = (j - 1u) % kDescBufs;
-            wait_vm(issued - (b == 0u ? desc_end0 : desc_end1));
-            const uint32_t base = desc_lds + b * 1024u;
-            SegDesc d;
-            d.msg = sid;
-            d.k = 0u;
-            d.off = *(const __attribute__((address_space(3))) uint64_t*)(uintptr_t)(
-                base + 8u * (uint32_t)lane);
-            d.len = *(const lds_u32*)(uintptr_t)(base + 512u + 4u * (uint32_t)lane);
-            d.seed = *(const lds_u32*)(uintptr_t)(base + 768u + 4u * (uint32_t)lane);
-            return d;
-        };
-        // setup_lane's geometry for k = 0, nseg = 1, into the producer's DMA
-        // sources and a group's fold fields; the sources are transposed by
-        // lane shuffles (slot 0, setup_lane's scratch, is in flight here)
-        auto setup_pipe = [&](const SegDesc& d, uint32_t gg, Fld& F) __attribute__((always_inline)) {
-            const uint32_t seg = gg * 64u + (uint32_t)lane;
-            bool valid = seg < total;
-            const uint32_t nseg = valid ? segments(d.len) : 0u;
-            long_seen |= __ballot(valid && nseg > 1u) != 0;  // left to the second pass
-            valid = valid && nseg <= 1u;
-            const SegGeom geo = seg_geom(arena + d.off, d.len, 0u, valid ? 1u : 0u, SEG);
-            const uint32_t nl = valid ? geo.nl : 0u;
-            F.valid = valid;
-            F.msg = d.msg;
-            F.R = max(wave_max(nl), 1u);
-            F.hskip = 0u;
-            if (kHornerSkip && F.R == 1u) {
-                const uint32_t sl0 = valid ? (uint32_t)(geo.S - geo.L0) : 128u;
-                F.hskip = __ballot(sl0 < 64u) == 0 ? 8u : 0u;
-            }
-            F.r0 = F.R - nl;
-            F.sl = valid ? (uint32_t)(geo.S - geo.L0) : 0u;
-            const uint64_t el = valid ? geo.E - geo.L0 : 0u;
-            F.lo_part = (F.sl & 15u) != 0;
-            F.hi_part = (el & 15u) != 0;
-            F.jE = (uint32_t)(el >> 7);
-            F.eE = (uint32_t)(el & 127u);
-            F.c0 = ~d.seed;
-            F.padE = valid ? (uint32_t)(geo.L0 + ((uint64_t)nl << 7) - geo.E) : 0u;
-            const uint32_t gS = F.sl >> 4;
-            const uint32_t gE = (uint32_t)((el + 15u) >> 4);
-            const uint32_t plo_l = 8u * F.r0 + gS;
-            const uint32_t pcnt_l = valid ? gE - gS : 0u;
-            const uint64_t pb_l = geo.L0 - ((uint64_t)F.r0 << 7);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {  // instruction i: segment 8i + lane/8 (dma_round)
-                const int src = 8 * i + (lane >> 3);
-                const uint32_t pp = ((uint32_t)lane & 7u) ^ ((4u * i + ((uint32_t)lane >> 4)) & 7u);
-                pbase[i] = shfl64(pb_l, src) + 16u * pp;
-                plo[i] = (uint32_t)__shfl((int)plo_l, src) - pp;
-                pcnt[i] = (uint32_t)__shfl((int)pcnt_l, src);
-            }
-        };
-        // the producer's next group, set up when its rounds are next (called
-        // before a wait, so the arithmetic overlaps the loads in flight)
-        auto prepare = [&]() __attribute__((always_inline)) {
-            if (p_r < p_R) {
-                return;
-            }
-            const uint32_t j = p_j + 1u;
-            const uint32_t gg = group_of(j);
-            if (gg >= ngroups) {
-                return;
-            }
-            const SegDesc d = desc_read(j);
-            desc_issue(j + kDescBufs);  // the buffer just read (the DMA waits for the reads)
-            if (nq == 0u) {
-                setup_pipe(d, gg, F1);
-                p_R = F1.R;
-            } else {
-                setup_pipe(d, gg, F2);
-                p_R = F2.R;
-            }
-            ++nq;
-            p_j = j;
-            p_r = 0u;
-        };
-        auto issue = [&]() __attribute__((always_inline)) {
-            if (p_r >= p_R) {
-                return;  // nothing left to load
-            }
-            const uint32_t slot = wave_lds + (pseq & 1u) * kSlotBytes;
-            if (!NT || (kShortDefaultPolicy && p_R <= 2u)) {
-                dma_round<false>(slot, pbase, plo, pcnt, zero, p_r);
-            } else {
-                dma_round<true>(slot, pbase, plo, pcnt, zero, p_r);
-            }
-            issued += 8u;
-            if (pseq & 1u) {
-                slot_end1 = issued;
-            } else {
-                slot_end0 = issued;
-            }
-            ++p_r;
-            ++pseq;
-        };
-        // one folded round: the next group's setup if due, the wait, the
-        // line's edges fixed and read, the slot refilled
-        auto step = [&](const Fld& F, uint32_t r, uint32_t (&m)[32]) __attribute__((always_inline)) {
-            prepare();
-            wait_vm(issued - ((cseq & 1u) ? slot_end1 : slot_end0));
-            const uint32_t slot = wave_lds + (cseq & 1u) * kSlotBytes;
-            const uint32_t j = r - F.r0;  // lanes before their stream wrap: no edge
-            const bool fx_lo = F.lo_part && j == 0u;
-            const bool fx_hi = F.hi_part && j == F.jE;
-            const bool fx_sd = F.valid && (j == 0u || (j == 1u && F.sl > 124u));
-            if (__ballot(fx_lo || fx_hi || fx_sd)) {
-                if (fx_lo || fx_hi || fx_sd) {
-                    line_fixup(slot, rd_off, fx_lo, F.sl, fx_hi, F.eE, fx_sd,
-                               (int)(F.sl - 128u * j), F.c0);
-                }
-            }
-#pragma unroll
-            for (int kk = 0; kk < 8; ++kk) {
-                const u32x4 v = *(lds_cu4*)(uintptr_t)(slot + (rd_off ^ (16u * kk)));
-                m[4 * kk + 0] = v.x;
-                m[4 * kk + 1] = v.y;
-                m[4 * kk + 2] = v.z;
-                m[4 * kk + 3] = v.w;
-            }
-            issue();
-            ++cseq;
-        };
-        if (gfirst < ngroups) {
-            setup_pipe(spec, gfirst, F0);  // the prologue's descriptors (identity)
-            p_R = F0.R;
-#pragma unroll
-            for (uint32_t j = 1; j <= kDescBufs; ++j) {
-                desc_issue(j);
-            }
-            issue();
-            prepare();
-            issue();
-            FOLD_STAMP(2)
-        }
-        for (uint32_t g = gfirst; g < ngroups; g += stride) {
-            const uint32_t R = F0.R;
-            uint32_t Rm[32];
-            if (R == 1u) {
-                step(F0, 0u, Rm);  // the remainder is the line
-            } else {
-                uint32_t q[32], p[32];
-                for (uint32_t r = 0; r + 1u < R; ++r) {
-                    uint32_t m[32];
-                    step(F0, r, m);
-                    if (r == 0u) {
-                        first_round(q, p, m);
-                    } else {
-                        fold_round(q, p, m);
-                    }
-                }
-                uint32_t H[32];
-                tail_taps(q, p, H);  // before the last line lands
-                uint32_t m[32];
-                step(F0, R - 1u, m);
-#pragma unroll
-                for (int d = 0; d < 32; ++d) {
-                    Rm[d] = m[d] ^ H[d];
-                }
-            }
-            const uint32_t crc = F0.hskip ? tail_horner<8>(Rm, tab_lds) : tail_horner(Rm, tab_lds);
-            // un-shift the zero padding after E, invert, store (one segment
-            // per message: no move, no combine)
-            uint32_t contrib = F0.valid ? crc : 0u;
-            if (__ballot(F0.padE != 0u) != 0 && F0.valid) {
-                contrib = gmul(crc, xneg8[F0.padE]);
-            }
-            if (F0.valid) {
-                a.out[F0.msg] = contrib ^ 0xffffffffu;
-            }
-            F0 = F1;
-            F1 = F2;
-            nq -= nq ? 1u : 0u;
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load outlives the loop
-    } else if constexpr (ONE) {
+    if constexpr (ONE) {
         // The speculative one-segment kernel: every group the same work, so
         // wave w of block b keeps round 3's static share, groups
         // g0 + j stride (the set its claims k = w, w + WPB, ... name, gid

@@ -678,20 +678,18 @@ def test_speculative_single_launch(cuda):
 
 @pytest.mark.parametrize("n", [1_000, 100_003, 600_000])
 def test_one_segment_pipeline_shapes(cuda, n):
-    """The one-segment kernel's rolling pipeline (round 5): a slot is
-    refilled with the next round of the wave's stream of groups -- the same
-    group's next line or the next group's first lines -- so consecutive
-    groups of different line counts (1 to 17 lines at 2 KiB segments) follow
-    each other in the slots, with descriptors loaded ahead by LDS-DMA (full
-    groups) or directly (the partial last group).  Declared bounds make every
-    batch ONE launch; 4-wave blocks (n = 1,000 and 100,003) and 8-wave
-    blocks (600,000); with and without seeds; blocks of one line count
-    alternate with mixed ones; a few messages past the bound go to the
-    second pass."""
+    """The one-segment kernel (every message declared to fit one segment):
+    consecutive groups of different line counts (1 to 17 lines at 2 KiB
+    segments) in a wave's sequence, the batch's partial last group, 4-wave
+    blocks (n = 1,000 and 100,003) and 8-wave blocks (600,000), with and
+    without seeds, contiguous 64/256-byte messages like the bench's, and a
+    few messages past the declared bound, folded by the second pass.  (Round
+    5 A/B'd a rolling two-slot pipeline for this kernel against these
+    shapes: correct, but not faster; DESIGN.md Appendix A.)"""
     import torch
     from blazingmq_amd.crc32c import last_launch
     rng = np.random.default_rng(94 + n)
-    arena_np = rng.integers(0, 256, size=80 << 20, dtype=np.uint8)
+    arena_np = rng.integers(0, 256, size=160 << 20, dtype=np.uint8)  # > 600,000 x 256 B
     arena = torch.from_numpy(arena_np).to(cuda)
     s = torch.cuda.Stream(cuda)
 
@@ -702,6 +700,8 @@ def test_one_segment_pipeline_shapes(cuda, n):
             np.cumsum(lens[:-1], out=offs[1:])
         else:
             offs = np.array(rng.integers(0, arena_np.size - lens.astype(np.int64) + 1), np.int64)
+        # device-pointer batches are not range-checked by the library: check here
+        assert int((offs + lens).max()) <= arena_np.size, tag
         sd = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64).astype(np.uint32)
         got = Crc32c.calculate_batch(arena, torch.from_numpy(offs).to(cuda),
                                      torch.from_numpy(lens.view(np.int32)).to(cuda),

@@ -2,7 +2,12 @@
 bmqcrc_reserve (the launch path allocates and synchronizes nothing), and
 concurrent batches on different streams from different host threads
 (per-(device, stream) workspaces, bmqp_crc32c.h:40-42 thread safety)."""
+import json
+import os
+import subprocess
+import sys
 import threading
+import time
 
 import numpy as np
 import pytest
@@ -280,3 +285,55 @@ def test_concurrent_gather_and_multi_device_walks(cuda):
         th.join(timeout=150)
     assert not any(th.is_alive() for th in threads), "a host-buffer call did not return"
     assert not errors, errors
+
+
+def test_processes_share_the_planner_on_one_gpu(cuda, record_property, tmp_path):
+    """Three processes CRC ragged batches of 1.4M+ messages on the same GPU at
+    once, with the default planner wait limit (tests/mp_planner_worker.py).
+    The single-pass planner's blocks meet grid-wide, so with other processes'
+    kernels resident a planner may give its map up (then the fold searches
+    the segment offsets, and the stream plans with the meeting-free pair for
+    a while): every CRC of every step must still match the oracle, and each
+    process's median step must stay within 1.3x of its share of the GPU
+    (3x one process's step alone; + 0.5 ms for the host's part of a step).
+    The given-up maps are recorded (test property plan_voided)."""
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "mp_planner_worker.py")
+
+    def launch(nproc, steps, tag):
+        sync = tmp_path / tag
+        sync.mkdir()
+        procs = [subprocess.Popen([sys.executable, worker, str(w), str(steps), str(sync)],
+                                  stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+                 for w in range(nproc)]
+        try:
+            deadline = time.time() + 180
+            while sum((sync / ("ready_%d" % w)).exists() for w in range(nproc)) < nproc:
+                assert all(p.poll() is None for p in procs), [p.stderr.read()[-2000:]
+                                                              for p in procs if p.poll()]
+                assert time.time() < deadline, "workers not ready"
+                time.sleep(0.05)
+            (sync / "go").touch()
+            res = []
+            for p in procs:
+                out, err = p.communicate(timeout=180)
+                assert p.returncode == 0, err[-3000:]
+                res.append(json.loads(out.strip().splitlines()[-1]))
+            return res
+        finally:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+                    p.wait()
+
+    alone = launch(1, 8, "alone")[0]
+    shared = launch(3, 8, "shared")
+    assert alone["mismatches"] == 0 and all(r["mismatches"] == 0 for r in shared), shared
+    share = 3 * alone["median_ms"]
+    worst = max(r["median_ms"] for r in shared)
+    record_property("alone_ms", round(alone["median_ms"], 3))
+    record_property("shared_ms", [round(r["median_ms"], 3) for r in shared])
+    record_property("plan_voided", [r["plan_voided"] for r in shared])
+    print("alone %.3f ms, three processes %s ms, given-up maps %s"
+          % (alone["median_ms"], [round(r["median_ms"], 3) for r in shared],
+             [r["plan_voided"] for r in shared]))
+    assert worst <= 1.3 * share + 0.5, (alone, shared)

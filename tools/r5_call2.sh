@@ -18,7 +18,7 @@ for v in base one4; do
     set -- $w
     rc=0
     line=$(timeout -k 10 180 python bench.py --config 1M_x_256B --msgs $1 --msg-bytes $2 --rotate 4 \
-        --steps 30 --warmup 5 --no-cpu-baseline 2> gpurun_out/r5/one_ab_$v_$1_$2.err | tail -1) || rc=$?
+        --steps 30 --warmup 5 --no-cpu-baseline 2> gpurun_out/r5/one_ab_${v}_$1_$2.err | tail -1) || rc=$?
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then cp /tmp/base.so $lib/libbmqcrc.so; echo "bench rc $rc"; exit $rc; fi
     echo "{\"variant\": \"$v\", \"msgs\": $1, \"bytes\": $2, \"bench\": $line}" >> $out
     echo "$v $1 x $2: $(echo "$line" | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["ms_per_step"], d["roofline"]["kernel_avg_us"], d["roofline"]["frac"], d["roofline"]["frac_per_step"], d["parity"])')"
