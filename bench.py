@@ -224,6 +224,20 @@ def cpu_baseline(lens_np, seed, seconds):
             ref.update({"reference_published_ns": ns, "reference_published_at": where,
                         "reference_published_host": "the reference's own (unnamed) 64-bit "
                                                     "build host"})
+        # the drop-in scalar bmqp::Crc32c::calculate (the product's CPU path,
+        # what unbatched callers link) in the same loop, same host
+        try:
+            import subprocess
+            exe = os.path.join(ROOT, "tools", "bin", "scalar_ladder")
+            line = subprocess.run([exe, str(size)], capture_output=True, text=True, timeout=60,
+                                  check=True).stdout.splitlines()[-1]
+            d = json.loads(line)
+            ref["dropin_calculate_ns"] = d["calculate_ns"]
+            ref["dropin_blob_4KiB_ns"] = d["blob_4KiB_ns"]
+            ref["dropin_source"] = "tools/bin/scalar_ladder (libbmqcrc.so, csrc/crc32c_cpu.cpp)"
+        except (OSError, subprocess.SubprocessError, ValueError, KeyError, IndexError) as e:
+            ref["dropin_calculate_ns"] = None
+            ref["dropin_error"] = str(e)[:200]
         res["reference_loop"] = ref
     return res
 

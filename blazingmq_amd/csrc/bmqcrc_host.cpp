@@ -1744,7 +1744,7 @@ uint64_t bmqcrc_host_fallbacks(int32_t* last_rc)
 
 uint32_t bmqcrc_version(void)
 {
-    return (2u << 16) | 5u;
+    return (2u << 16) | 6u;
 }
 
 }  // extern "C"

@@ -63,7 +63,9 @@ extern "C" {
 
 typedef struct bmqcrc_opts {
     uint32_t struct_size; /* sizeof(bmqcrc_opts); 0 reads the ABI 2.0 fields only (device,
-                             stream, flags, seg_bytes): set it to use anything later */
+                             stream, flags, seg_bytes): set it to use anything later
+                             (ABI 2.6: 0 with ndevices, max_len or min_len set is
+                             BMQCRC_EINVAL, where 2.1-2.4 read the whole struct) */
     int32_t device;       /* HIP device ordinal; -1 = current device */
     void* stream;         /* hipStream_t; NULL = that device's default (null) stream */
     uint32_t flags;       /* BMQCRC_F_* */
@@ -246,7 +248,7 @@ const char* bmqcrc_last_error(void);
 void bmqcrc_note_host_fallback(int32_t rc);
 uint64_t bmqcrc_host_fallbacks(int32_t* last_rc);
 
-/* ABI version: (major << 16) | minor (2.5). */
+/* ABI version: (major << 16) | minor (2.6). */
 uint32_t bmqcrc_version(void);
 
 #ifdef __cplusplus

@@ -11,7 +11,7 @@
 // splits the same bytes into 4 KiB buffers (the SDK/broker blob buffer size,
 // bmqt_sessionoptions.cpp:37) and chains them like bmqp_crc32c.cpp:47-67.
 //
-//   tools/bin/scalar_ladder            one JSON line per size
+//   tools/bin/scalar_ladder [SIZE ...]  one JSON line per size (default: the ladder)
 #include "bmqp_crc32c.h"
 
 #include <stdio.h>
@@ -56,7 +56,7 @@ static double ns_per_call(F&& f, int* iters_out)
     return dt * 1e9 / iters;
 }
 
-int main()
+int main(int argc, char** argv)
 {
     const int ladder[] = {11,    16,    21,     59,     64,      69,      251,      256,
                           261,   1019,  1024,   1029,   4091,    4096,    4101,     16379,
@@ -64,7 +64,14 @@ int main()
     const int k_MAX = 67108864;
     std::vector<char> buffer(k_MAX);
     std::generate_n(buffer.begin(), k_MAX, rand);
-    for (int length : ladder) {
+    std::vector<int> sizes(ladder, ladder + sizeof ladder / sizeof ladder[0]);
+    if (argc > 1) {
+        sizes.clear();
+        for (int i = 1; i < argc; ++i) {
+            sizes.push_back(std::max(0, std::min(k_MAX, atoi(argv[i]))));
+        }
+    }
+    for (int length : sizes) {
         int iters = 0, biters = 0;
         const double ns = ns_per_call([&] { return Crc32c::calculate(buffer.data(), length); },
                                       &iters);
