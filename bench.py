@@ -186,10 +186,16 @@ def cpu_baseline(lens_np, seed, seconds):
     nbytes = int(lens.sum(dtype=np.uint64))
     arena = oracle.fill_payload(0, nbytes, seed)
     t1, reps1 = oracle.time_batch_for(arena, offs, lens, 1, "hw", 0.5)
-    t, reps = oracle.time_batch_for(arena, offs, lens, threads, "hw", max(0.5, seconds))
+    # the multi-threaded leg shares the box's host with other jobs: three
+    # timed windows, the best one reported (interference only slows a
+    # window), all three listed
+    legs = [oracle.time_batch_for(arena, offs, lens, threads, "hw", max(0.5, seconds) / 3)
+            for _ in range(3)]
     gib = nbytes / 2**30
+    t, reps = min(legs, key=lambda tr: tr[0] / tr[1])
     res = {
         "value": round(gib * reps / t, 3),
+        "windows_GiBps": [round(gib * r / tt, 3) for tt, r in legs],
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
@@ -201,9 +207,11 @@ def cpu_baseline(lens_np, seed, seconds):
                         % ((os.cpu_count() or 8) // 8, os.cpu_count() or 0, threads),
         "sample": "first %d msgs (%.0f MiB) of the same synthetic batch; %d threads (this "
                   "GPU's share of the host: OMP_NUM_THREADS, 16 per GPU on the pool), created "
-                  "once before the clock, %d warm passes (%.2f s); single thread %d warm passes "
-                  "(%.2f s) = %.2f GiB/s; SSE4.2 crc32q 3-way interleaved (bdlde::Crc32c "
-                  "default analogue, oracle/crc32c_oracle.c); host %s, nproc %d"
+                  "once before the clock, best of three windows: %d warm passes (%.2f s); "
+                  "single thread %d warm passes "
+                  "(%.2f s) = %.2f GiB/s; SSE4.2 crc32q 3-way interleaved, lanes joined by "
+                  "shift tables (bdlde::Crc32c default analogue, oracle/crc32c_oracle.c); "
+                  "host %s, nproc %d"
                   % (n, gib * 1024, threads, reps, t, reps1, t1, gib * reps1 / t1, cpu_model(),
                      os.cpu_count()),
     }
