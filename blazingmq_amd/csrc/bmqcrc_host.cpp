@@ -461,6 +461,15 @@ int run_batch(Ctx& c, uint32_t flags, uint32_t seg, const void* arena, uint64_t 
             a.spec = hint_u;
         }
     }
+    if ((kTuneBits & 4096u) && !a.whole && a.map_planned && w->hint_host &&
+        ((flags & BMQCRC_F_PLAN) ||
+         (__atomic_load_n(w->hint_host, __ATOMIC_RELAXED) & 0xffu) == kHintUnknown)) {
+        // A/B only (TUNE bit 12): a batch planned without a shape prediction
+        // (BMQCRC_F_PLAN, or no history on the stream) gets the light k_plan
+        // (counts and closed forms, no size-class map); a ragged one is then
+        // folded by searching seg_first, and the stream learns its shape
+        a.map_planned = 0;
+    }
     if ((kTuneBits & 2048u) && !a.whole && (flags & BMQCRC_F_PLAN) &&
         spec_eligible(c, n, a.blocks_per_cu)) {
         // A/B only (TUNE bit 11): a batch with no shape history launched as

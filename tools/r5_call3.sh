@@ -35,3 +35,8 @@ for w in "1048576 256" "2097152 256" "4194304 256" "4194304 64" "2097152 128"; d
       --no-cpu-baseline > gpurun_out/r5/prof_$tag.log 2>&1 || exit $?
   tail -1 gpurun_out/r5/prof_$tag.log | cut -c1-300
 done
+# final-build evidence: per-config bench lines, kernel traces and FETCH/WRITE
+# passes (profiles/r05), the shard forecast, the smoke
+timeout -k 10 1500 bash tools/profile_round.sh r5 64k_x_64KiB 1M_x_256B 16_x_256MiB zipf_4M 1k_x_4KiB \
+    > gpurun_out/r5/profile_round.log 2>&1 || exit $?
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r5/smoke.log 2>&1
