@@ -461,13 +461,19 @@ int run_batch(Ctx& c, uint32_t flags, uint32_t seg, const void* arena, uint64_t 
             a.spec = hint_u;
         }
     }
-    if ((kTuneBits & 4096u) && !a.whole && a.map_planned && w->hint_host &&
-        ((flags & BMQCRC_F_PLAN) ||
-         (__atomic_load_n(w->hint_host, __ATOMIC_RELAXED) & 0xffu) == kHintUnknown)) {
-        // A/B only (TUNE bit 12): a batch planned without a shape prediction
-        // (BMQCRC_F_PLAN, or no history on the stream) gets the light k_plan
-        // (counts and closed forms, no size-class map); a ragged one is then
-        // folded by searching seg_first, and the stream learns its shape
+    if (!(kTuneBits & (16u | 4096u)) && !a.whole && !a.spec && a.map_planned && w->hint_host &&
+        (__atomic_load_n(w->hint_host, __ATOMIC_RELAXED) & 0xffu) != kHintRagged &&
+        !(host_max_len != UINT64_MAX && host_max_len > a.seg_bytes &&
+          (host_min_len == 0 || (host_min_len - 1) / a.seg_bytes != (host_max_len - 1) / a.seg_bytes))) {
+        // Planned with no evidence that the batch is ragged -- no shape
+        // history on the stream, or BMQCRC_F_PLAN after a closed-form batch
+        // (segment counts seen on the host decide for host batches): the
+        // light k_plan (counts and closed forms, no size-class map).  A
+        // ragged batch is then folded by searching seg_first, and k_fold
+        // records its shape, so the stream's next batch gets the map
+        // (planned steps: 1M x 256 B 0.055 against 0.066 ms, 1k x 4 KiB 0.013
+        // against 0.017; a ragged first batch 1.09x: Zipf 4.45 against 4.07;
+        // profiles/r05/ab/light_planner.jsonl; TUNE bit 12 restores round 4)
         a.map_planned = 0;
     }
     if ((kTuneBits & 2048u) && !a.whole && (flags & BMQCRC_F_PLAN) &&

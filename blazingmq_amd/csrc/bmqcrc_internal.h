@@ -32,8 +32,8 @@ constexpr int kBuckets = 16;            // segment size classes: floor(log2(line
 // instead of one 8-wave block claiming groups dynamically (A/B), bit11
 // launches BMQCRC_F_PLAN batches as the speculative one-segment kernel instead
 // of planning them (the cost of speculating on a stream with no history),
-// bit12 plans a batch with no shape history with the light k_plan (no
-// size-class map) instead of k_plan_map.
+// bit12 plans every batch that is planned at all with k_plan_map (round 4)
+// instead of the light k_plan when nothing says it is ragged.
 #ifndef BMQCRC_TUNE_BITS
 #define BMQCRC_TUNE_BITS 0u
 #endif

@@ -870,6 +870,11 @@ __device__ unsigned long long g_fold_trace[kFoldTraceWaves][8];
 #define FOLD_STAMP(k)
 #endif
 
+#ifndef BMQCRC_ONE_DIAG
+#define BMQCRC_ONE_DIAG 0  // diagnostic builds of the ONE kernel (wrong CRCs): bit 0 skips the
+                           // remainder step, bit 1 the fold; product: 0
+#endif
+
 #ifndef BMQCRC_SNAKE
 #define BMQCRC_SNAKE 1  // 0: every round in block order (A/B)
 #endif
@@ -1191,6 +1196,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     // carried through the loop) gives the remainder words Rm.
     auto fold_rounds = [&](const Group& G, uint32_t (&Rm)[32]) {
         uint32_t q[32], p[32];
+        [[maybe_unused]] uint32_t sink = 0;  // BMQCRC_ONE_DIAG & 2: keeps the line reads
         const uint32_t R = G.R;
         auto load_line = [&](uint32_t r, uint32_t slot, uint32_t (&m)[32]) {
             // Byte edges of this round's line: the piece cut by S (first line),
@@ -1224,7 +1230,12 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
             if (r + 2 < R) {
                 dma_round<NT>(slot, G.pbase, G.plo, G.pcnt, zero, r + 2);
             }
-            if (r == 0) {
+            if (ONE && (BMQCRC_ONE_DIAG & 2)) {
+#pragma unroll
+                for (int d = 0; d < 32; ++d) {
+                    sink ^= m[d];
+                }
+            } else if (r == 0) {
                 first_round(q, p, m);
             } else {
                 fold_round(q, p, m);
@@ -1245,7 +1256,14 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
             return;
         }
         uint32_t H[32];
-        tail_taps(q, p, H);
+        if (ONE && (BMQCRC_ONE_DIAG & 2)) {
+#pragma unroll
+            for (int d = 0; d < 32; ++d) {
+                H[d] = d == 0 ? sink : 0u;
+            }
+        } else {
+            tail_taps(q, p, H);
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         uint32_t m[32];
         load_line(R - 1u, slot, m);
@@ -1460,7 +1478,16 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
                                    uni, sorted, ep);
                 issue_first_rounds(G);
             }
-            finish(C, C.hskip ? tail_horner<8>(Rm, tab_lds) : tail_horner(Rm, tab_lds));
+            if (BMQCRC_ONE_DIAG & 1) {  // diagnostic: no remainder step (wrong CRCs)
+                uint32_t x = 0;
+#pragma unroll
+                for (int d = 0; d < 32; ++d) {
+                    x ^= Rm[d];
+                }
+                finish(C, x);
+            } else {
+                finish(C, C.hskip ? tail_horner<8>(Rm, tab_lds) : tail_horner(Rm, tab_lds));
+            }
         }
     } else {
     uint32_t g = gid(wave), g1 = ngroups, g2 = ngroups;  // (= gfirst)
