@@ -875,6 +875,11 @@ __device__ unsigned long long g_fold_trace[kFoldTraceWaves][8];
                            // remainder step, bit 1 the fold; product: 0
 #endif
 
+#ifndef BMQCRC_SHORT_NT_WHOLE_LINES
+#define BMQCRC_SHORT_NT_WHOLE_LINES 1  // 0: every short group with the default policy (round 4)
+#endif
+constexpr bool kShortNtWholeLines = BMQCRC_SHORT_NT_WHOLE_LINES != 0;
+
 #ifndef BMQCRC_SNAKE
 #define BMQCRC_SNAKE 1  // 0: every round in block order (A/B)
 #endif
@@ -1076,6 +1081,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
         uint64_t E, L0, mend;
         uint32_t msg, k, nseg, nl, R, r0, sl, jE, eE, c0, hskip;
         bool valid, first, lo_part, hi_part;
+        bool whole_lines;  // every valid lane's [S, E) starts and ends on a 128-byte line
     };
     // Geometry of one lane's segment k of a message of nseg segments.
     auto setup_lane = [&](bool valid, uint32_t msg, uint32_t k, uint32_t nseg, uint64_t off,
@@ -1112,6 +1118,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
         G.jE = (uint32_t)(el >> 7);    // line holding E's cut piece
         G.eE = (uint32_t)(el & 127u);  // E's offset in that line
         G.c0 = ~seed;
+        G.whole_lines = __ballot(G.valid && (((geo.S | geo.E) & 127u) != 0)) == 0;
         // DMA source per instruction: pieces [gS, gE) of the stream overlap
         // [S, E); the stream piece index in round r is 8 (r - r0) + piece
         const uint32_t gS = G.sl >> 4;
@@ -1173,12 +1180,18 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
                        d.seed, G);
         }
     };
-    // Load policy per group: a group of one or two lines per lane (small
-    // messages) reads with the default policy, longer streams non-temporally.
-    // Measured on MI355X: the default policy is 3 %
-    // faster on 1M x 256 B and 8-10 % slower on every config of long streams.
+    // Load policy per group: streams of three or more lines read
+    // non-temporally; a group of one or two lines per lane does too when every
+    // lane's segment is whole lines (no line shared with a neighbouring
+    // message), else with the default policy, which keeps a line that two
+    // messages share in L2 for the second.  Measured on MI355X batches read
+    // from HBM (profiles/r05/ab/ntshort_ab.jsonl): non-temporal 256-byte
+    // messages +13-15 % (4M: 0.640 -> 0.721 of the roofline), 128-byte +5 %,
+    // 64-byte flat, 200-byte (lines shared) -8 %; long streams 8-10 % faster
+    // non-temporal (round 2).  Round 2 chose the default policy for every
+    // short group from a batch the Infinity Cache held (+3 %).
     auto issue_first_rounds = [&](const Group& G) {
-        if (!NT || (kShortDefaultPolicy && G.R <= 2u)) {
+        if (!NT || (kShortDefaultPolicy && G.R <= 2u && !(kShortNtWholeLines && G.whole_lines))) {
             dma_round<false>(wave_lds, G.pbase, G.plo, G.pcnt, zero, 0);
             if (G.R > 1) {
                 dma_round<false>(wave_lds + kSlotBytes, G.pbase, G.plo, G.pcnt, zero, 1);
