@@ -60,6 +60,7 @@ __constant__ uint32_t c_x2col[31][32] = BMQCRC_X2COL;
 __constant__ uint32_t c_xneg8[136] = BMQCRC_XNEG8;
 __constant__ uint32_t c_xbytes[4][256] = BMQCRC_XBYTES;
 __constant__ uint32_t c_ty[8][256] = BMQCRC_TY;
+__constant__ uint32_t c_rtab11[6144] = BMQCRC_RTAB11;
 
 // All-zero line in device memory: the LDS-DMA source of every 16-byte piece
 // that lies outside a segment's bytes, and of every round outside its stream.
@@ -394,6 +395,51 @@ __device__ __forceinline__ uint32_t tail_horner(const uint32_t (&R)[32], uint32_
         c = xor3(hi, lo, tab_lookup(tab_lds, 7, v >> 24) ^ tab_lookup(tab_lds, 3, w >> 24));
     }
     return c;
+}
+
+// The same reduction with 11-bit slices (k_fold's 8-wave blocks, which have
+// the LDS for them: 24 KiB, kTab11Bytes).  One word per step, c <- (c ^ R_d)
+// * y, in three lookups (word bits 2-12, 13-23, and 24-31 with 0-1, each
+// slice's byte offset formed by one AND, or a shift or rotate and an AND),
+// against four per word with byte slices: 100 lookups per segment instead of
+// 128, and no more VALU.  Two independent chains keep the dependent depth at
+// 16 steps: A over words 0-15, B over 16-31, raw = A * y^16 + B, the join by
+// four byte lookups.  SKIP = 8: words 0-15 are zero in every lane (chain A
+// and the join drop out).
+constexpr uint32_t kTab11Bytes = 6144 * 4;
+constexpr uint32_t kT11Hi = 8192, kT11Top = 16384, kT11Join = 20480;  // slice offsets (bytes)
+
+__device__ __forceinline__ uint32_t step11(uint32_t c, uint32_t r, uint32_t tab_lds)
+{
+    const uint32_t v = c ^ r;
+    const uint32_t a0 = v & 0x1ffcu;
+    const uint32_t a1 = (v >> 11) & 0x1ffcu;
+    const uint32_t a2 = __builtin_amdgcn_alignbit(v, v, 22) & 0xffcu;  // rotr 22: bits 24-31, 0-1
+    return xor3(*(const lds_u32*)(uintptr_t)(tab_lds + a0),
+                *(const lds_u32*)(uintptr_t)(tab_lds + kT11Hi + a1),
+                *(const lds_u32*)(uintptr_t)(tab_lds + kT11Top + a2));
+}
+
+template <int SKIP = 0>
+__device__ __forceinline__ uint32_t tail_chains11(const uint32_t (&R)[32], uint32_t tab_lds)
+{
+    static_assert(SKIP == 0 || SKIP == 8, "chain A runs whole or not at all");
+    uint32_t ca = 0, cb = 0;
+#pragma unroll
+    for (int d = 0; d < 16; ++d) {
+        if (SKIP == 0) {
+            ca = step11(ca, R[d], tab_lds);
+        }
+        cb = step11(cb, R[16 + d], tab_lds);
+    }
+    if (SKIP != 0) {
+        return cb;
+    }
+    const uint32_t j = tab_lds + kT11Join;
+    return xor3(cb, *(const lds_u32*)(uintptr_t)(j + 4u * (ca & 0xffu)),
+                *(const lds_u32*)(uintptr_t)(j + 1024u + 4u * ((ca >> 8) & 0xffu))) ^
+           xor3(*(const lds_u32*)(uintptr_t)(j + 2048u + 4u * ((ca >> 16) & 0xffu)),
+                *(const lds_u32*)(uintptr_t)(j + 3072u + 4u * (ca >> 24)), 0u);
 }
 
 // Word w (0..31) of this lane's 128-byte line in an LDS slot (the pieces are
@@ -885,6 +931,16 @@ constexpr bool kShortNtWholeLines = BMQCRC_SHORT_NT_WHOLE_LINES != 0;
 #endif
 constexpr bool kSnakeRounds = BMQCRC_SNAKE != 0;
 
+#ifndef BMQCRC_TWO_ENDED
+#define BMQCRC_TWO_ENDED 0  // 1: claims from both ends of each block's groups (A/B)
+#endif
+constexpr bool kTwoEnded = BMQCRC_TWO_ENDED != 0;
+
+#ifndef BMQCRC_HORNER11
+#define BMQCRC_HORNER11 1  // 0: byte-sliced remainder tables in every block shape (round 4; A/B)
+#endif
+constexpr bool kHorner11 = BMQCRC_HORNER11 != 0;
+
 // Groups whose speculative first pass skipped a message (a block's list for
 // the second pass; past this many the second pass scans the block's groups).
 constexpr uint32_t kLongListCap = 64;
@@ -905,22 +961,38 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
 {
     constexpr uint32_t kThreads = WPB * 64;
     constexpr int kLds = WPB * kSlots * kSlotBytes;
+    // 11-bit remainder slices in the 8-wave blocks (one per CU: 159 KiB of
+    // LDS with them); 4-wave blocks, two of which share a CU, keep the 8 KiB
+    // byte slices
+    constexpr bool H11 = kHorner11 && WPB == 8;
+    constexpr int kTab = H11 ? (int)kTab11Bytes : kTabBytes;
     // remainder tables, DMA slots, move factors (not needed by ONE: no moves
     // in its first pass)
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kTabBytes + kLds + (ONE ? 0 : kXbBytes)];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kTab + kLds + (ONE ? 0 : kXbBytes)];
     // group claims (gid below): wave w starts with claim k = w, later k come
     // from this counter; long_n / long_list: the block's groups with a message
     // its speculative first pass skipped
     __shared__ uint32_t claim_ctr, long_n;
+    __shared__ unsigned long long claim2;  // two-ended claims: front count | back count << 32
     __shared__ uint32_t long_list[kLongListCap];
 
     const int lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t tab_lds = (uint32_t)(uintptr_t)(lds_u8*)lds;
-    const uint32_t wave_lds = tab_lds + kTabBytes + wave * (kSlots * kSlotBytes);
-    const uint32_t xb_lds = tab_lds + kTabBytes + kLds;
+    const uint32_t wave_lds = tab_lds + kTab + wave * (kSlots * kSlotBytes);
+    const uint32_t xb_lds = tab_lds + kTab + kLds;
+    // a segment's raw CRC from its 32 remainder words (skip: words 0-15 are
+    // zero in every lane; a wave-uniform choice between two compiled copies)
+    auto remainder = [&](const uint32_t (&Rm)[32], bool skip) -> uint32_t {
+        if constexpr (H11) {
+            return skip ? tail_chains11<8>(Rm, tab_lds) : tail_chains11(Rm, tab_lds);
+        } else {
+            return skip ? tail_horner<8>(Rm, tab_lds) : tail_horner(Rm, tab_lds);
+        }
+    };
     if (threadIdx.x == 0) {
         claim_ctr = WPB;
+        claim2 = 0ull;
         long_n = 0;
     }
 
@@ -928,13 +1000,17 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     // wait -- the remainder tables, k_plan's block words and the first group's
     // descriptors as if segment = message (true for BMQCRC_F_WHOLE_MESSAGES
     // and for identity batches; discarded otherwise).
-    constexpr int kTw = 2048 / kThreads, kXw = 1024 / kThreads;  // table words per thread
-    static_assert(kTw * kThreads == 2048 && kXw * kThreads == 1024, "table fill");
+    constexpr int kTw = (kTab / 4) / (int)kThreads, kXw = 1024 / kThreads;  // table words per thread
+    static_assert(kTw * (int)kThreads * 4 == kTab && kXw * kThreads == 1024, "table fill");
     uint32_t tw[kTw];
 #pragma unroll
     for (int i = 0; i < kTw; ++i) {
         const uint32_t t = threadIdx.x + (uint32_t)i * kThreads;
-        tw[i] = c_ty[t >> 8][t & 255u];
+        if constexpr (H11) {
+            tw[i] = c_rtab11[t];
+        } else {
+            tw[i] = c_ty[t >> 8][t & 255u];
+        }
     }
     uint32_t xw[kXw];
     if (!ONE) {
@@ -1060,15 +1136,44 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     };
     // a claim in two halves: the LDS atomic (lane 0) is issued early and its
     // result read later, so its latency hides behind other LDS work
+    // Two-ended claims (BMQCRC_TWO_ENDED, A/B): the block's K claims k =
+    // 0 .. K-1 are taken from both ends at once, waves 0 .. WPB/2-1 from the
+    // front (the map's first size classes), the others from the back (its
+    // last), so that a CU folds large and small groups side by side instead
+    // of one size class after another; one 64-bit LDS counter holds both
+    // counts, and a claim is valid while they sum to less than K.
+    const bool back = kTwoEnded && wave >= (uint32_t)WPB / 2u;
+    uint32_t kb = 0;  // this block's claims (gid(k) < ngroups exactly for k < kb)
+    if (kTwoEnded) {
+        const uint32_t full = ngroups / (nbk * (uint32_t)WPB);
+        kb = full * (uint32_t)WPB;
+        const uint32_t b = (kSnakeRounds && !ONE && (full & 1u)) ? nbk - 1u - blockIdx.x : blockIdx.x;
+        const uint64_t c = (uint64_t)(b + nbk * full) * WPB;
+        if (c < ngroups) {
+            kb += (uint32_t)min((uint64_t)WPB, (uint64_t)ngroups - c);
+        }
+    }
     auto claim_issue = [&]() {
-        uint32_t k = 0;
+        unsigned long long k = 0;
         if (lane == 0) {
-            k = atomicAdd(&claim_ctr, 1u);
+            if (kTwoEnded) {
+                k = atomicAdd(&claim2, back ? (1ull << 32) : 1ull);
+            } else {
+                k = atomicAdd(&claim_ctr, 1u);
+            }
         }
         return k;
     };
-    auto claim_take = [&](uint32_t k) {
-        return gid((uint32_t)__builtin_amdgcn_readfirstlane((int)k));
+    auto claim_take = [&](unsigned long long k) {
+        if (kTwoEnded) {
+            const uint32_t f = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)k);
+            const uint32_t bk = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(k >> 32));
+            if ((uint64_t)f + bk >= kb) {
+                return ngroups;
+            }
+            return gid(back ? kb - 1u - bk : f);
+        }
+        return gid((uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)k));
     };
     auto claim = [&]() { return claim_take(claim_issue()); };
     const uint32_t seg_shift = (SEG & (SEG - 1u)) == 0 ? (uint32_t)__builtin_ctz(SEG) : 0u;
@@ -1403,7 +1508,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
                     issue_first_rounds(H);
                     uint32_t Rm[32];
                     fold_rounds(H, Rm);
-                    uint32_t x = contribution(H, tail_horner(Rm, tab_lds));
+                    uint32_t x = contribution(H, remainder(Rm, false));
 #pragma unroll
                     for (int o = 32; o > 0; o >>= 1) {
                         x ^= (uint32_t)__shfl_xor((int)x, o);
@@ -1499,11 +1604,11 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
                 }
                 finish(C, x);
             } else {
-                finish(C, C.hskip ? tail_horner<8>(Rm, tab_lds) : tail_horner(Rm, tab_lds));
+                finish(C, remainder(Rm, C.hskip != 0u));
             }
         }
     } else {
-    uint32_t g = gid(wave), g1 = ngroups, g2 = ngroups;  // (= gfirst)
+    uint32_t g = kTwoEnded ? claim() : gid(wave), g1 = ngroups, g2 = ngroups;  // (= gfirst)
     if (g < ngroups) {
         g1 = claim();
         g2 = g1 < ngroups ? claim() : ngroups;
@@ -1515,7 +1620,11 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
                 r0 = resolve_sorted(r0, s0 < total);
             }
         }
-        const SegDesc d0 = identity ? spec : fetch_desc(a, r0, s0 < total);
+        // (the prologue's descriptors are gfirst's, the first claim's only
+        // with one-ended claims)
+        const SegDesc d0 = (identity && !kTwoEnded)
+                               ? spec
+                               : fetch_desc(a, identity ? SegRef{s0, 0u} : r0, s0 < total);
         const uint32_t s1 = g1 * 64u + (uint32_t)lane;
         const bool v1 = g1 < ngroups && s1 < total;
         SegRef r1 = map_segment(a, &pl, s1, v1, identity, uni, sorted, ep);
@@ -1534,7 +1643,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
         // the claim of the group after g2, issued before this group's fold
         // (whose LDS reads cover the atomic's latency), taken below
         const bool more = g1 < ngroups && g2 < ngroups;  // claims only grow: none left
-        const uint32_t k3 = more ? claim_issue() : 0u;
+        const unsigned long long k3 = more ? claim_issue() : 0ull;
         uint32_t Rm[32];
         fold_rounds(G, Rm);
         if (first_group) {
@@ -1561,7 +1670,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
             ref2 = map_segment(a, &pl, s3, g3 < ngroups && s3 < total, identity, uni, sorted, ep);
             issue_first_rounds(G);
         }
-        finish(C, C.hskip ? tail_horner<8>(Rm, tab_lds) : tail_horner(Rm, tab_lds));
+        finish(C, remainder(Rm, C.hskip != 0u));
         g = g1;
         g1 = g2;
         g2 = g3;

@@ -194,6 +194,45 @@ def horner_words(words, skip=0):
     return c
 
 
+T11 = G.remainder_tables11()
+
+
+def chains11(words, skip=False):
+    """k_fold's tail_chains11 (8-wave blocks): 11/11/10-bit slices, one word
+    per step, chain A over words 0-15 and B over 16-31, raw = A * y^16 + B.
+    The slice offsets are formed as the kernel forms them: v & 0x1ffc,
+    (v >> 11) & 0x1ffc and rotr(v, 22) & 0xffc (byte offsets into the
+    tables)."""
+    def step(c, r):
+        v = c ^ r
+        rot = ((v >> 22) | (v << 10)) & 0xFFFFFFFF
+        return (T11[(v & 0x1FFC) >> 2] ^ T11[2048 + (((v >> 11) & 0x1FFC) >> 2)] ^
+                T11[4096 + ((rot & 0xFFC) >> 2)])
+    ca = cb = 0
+    for d in range(16):
+        if not skip:
+            ca = step(ca, words[d])
+        cb = step(cb, words[16 + d])
+    if skip:
+        return cb
+    j = 0
+    for k in range(4):
+        j ^= T11[5120 + 256 * k + ((ca >> (8 * k)) & 0xFF)]
+    return j ^ cb
+
+
+def test_chains11_match_horner():
+    rng = np.random.default_rng(11)
+    for _ in range(300):
+        words = [int(w) for w in rng.integers(0, 2**32, size=32, dtype=np.uint64)]
+        assert chains11(words) == horner_words(words)
+        zero_a = [0] * 16 + words[16:]
+        assert chains11(zero_a, skip=True) == chains11(zero_a) == horner_words(zero_a, 8)
+    for w in (0, 1, 3, 0x80000000, 0xFFFFFFFF, 0x00FFE000, 0xFF000003):
+        words = [w] * 32
+        assert chains11(words) == horner_words(words)
+
+
 def test_one_line_horner_skip():
     # One-line groups: the remainder is the line, and words before the lowest
     # S of the wave are zero, so hskip = min(sl) // 8 steps can be skipped.

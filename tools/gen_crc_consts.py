@@ -22,6 +22,11 @@ Constants produced:
 * ``XBYTES[4][256]``: x^(8 * b * 256^i) mod P, the factor that moves a CRC
   past b * 256^i zero bytes; a segment's move to its message end multiplies
   the factors of the bytes of its distance (k_fold).
+* ``TY[8][256]``: byte-sliced "multiply by y" and "by y^2" tables for the
+  remainder reduction of 4-wave k_fold blocks (two words per Horner step).
+* ``RTAB11[6144]``: the same reduction in three 11/11/10-bit slices (one word
+  per step, two 16-word chains) plus the byte tables of the join by y^16,
+  for the 8-wave blocks: 3 lookups per word instead of 4.
 """
 import os
 import sys
@@ -90,6 +95,36 @@ def min_poly_of_y():
     raise AssertionError("no relation")
 
 
+def remainder_tables11():
+    """11-bit remainder tables (two 16-word chains, k_fold's 8-wave blocks):
+    [0][i] = (i << 2) * y, [1][i] = (i << 13) * y (2048 entries each: word
+    bits 2-12 and 13-23), [2][i] = (((i & 0xff) << 24) | (i >> 8)) * y (1024:
+    bits 24-31 and 0-1), then the join y^16: [k][b] = (b << 8k) * y^16; one
+    flat list of 6144 words, self-checked."""
+    one_r = 1 << 31
+    x32_r = one_r
+    for _ in range(32):
+        x32_r = mulmod_r(x32_r, 1 << 30)
+    y16_r = one_r
+    for _ in range(16):
+        y16_r = mulmod_r(y16_r, x32_r)
+    t11 = ([mulmod_r(i << 2, x32_r) for i in range(2048)] +
+           [mulmod_r(i << 13, x32_r) for i in range(2048)] +
+           [mulmod_r(((i & 0xff) << 24) | (i >> 8), x32_r) for i in range(1024)] +
+           [mulmod_r(b << (8 * k), y16_r) for k in range(4) for b in range(256)])
+    assert len(t11) == 6144
+    # the three fields cover every bit of a word once: T0 ^ T1 ^ T2 = v * y
+    for v in (0, 1, 0x80000000, 0xdeadbeef, 0x12345678, 0xffffffff):
+        got = (t11[(v >> 2) & 0x7ff] ^ t11[2048 + ((v >> 13) & 0x7ff)] ^
+               t11[4096 + (((v >> 24) & 0xff) | ((v & 3) << 8))])
+        assert got == mulmod_r(v, x32_r)
+        j = 0
+        for k in range(4):
+            j ^= t11[5120 + 256 * k + ((v >> (8 * k)) & 0xff)]
+        assert j == mulmod_r(v, y16_r)
+    return t11
+
+
 def main(out_path):
     # P = (x+1) * Q31, Q31 primitive (2^31-1 is prime) -> ord(x) = 2^31-1.
     assert pmod(P_NORMAL, 0b11) == 0
@@ -136,6 +171,7 @@ def main(out_path):
     y2_r = mulmod_r(x32_r, x32_r)
     ty = [[mulmod_r(b << (8 * (k % 4)), x32_r if k < 4 else y2_r) for b in range(256)]
           for k in range(8)]
+    t11 = remainder_tables11()
     with open(out_path, "w") as f:
         f.write("// GENERATED by tools/gen_crc_consts.py -- do not edit.\n")
         f.write("#pragma once\n#include <stdint.h>\n\n")
@@ -160,6 +196,12 @@ def main(out_path):
         f.write("#define BMQCRC_TY { \\\n")
         for k in range(8):
             f.write("  {%s}%s \\\n" % (", ".join("0x%08xu" % c for c in ty[k]), "," if k < 7 else ""))
+        f.write("}\n\n")
+        f.write("// 11-bit remainder tables and the y^16 join (6144 words, see gen_crc_consts.py)\n")
+        f.write("#define BMQCRC_RTAB11 { \\\n")
+        for i in range(0, 6144, 8):
+            f.write("  %s%s \\\n" % (", ".join("0x%08xu" % c for c in t11[i:i + 8]),
+                                    "," if i + 8 < 6144 else ""))
         f.write("}\n")
     print("wrote", out_path, "taps", taps)
 
