@@ -442,6 +442,66 @@ __device__ __forceinline__ uint32_t tail_chains11(const uint32_t (&R)[32], uint3
                 *(const lds_u32*)(uintptr_t)(j + 3072u + 4u * (ca >> 24)), 0u);
 }
 
+// The 32 remainder words reduced further at BYTE granularity before any
+// lookup (BMQCRC_BYTE_FOLD, A/B).  The minimal polynomial of z = x^8 is P
+// itself (as for y = x^32: x^8 and x^32 are Frobenius conjugates of x), so the
+// remainder's 128 bytes b_i (raw = sum b_i z^(131-i)) reduce with the same 17
+// taps at byte lags 32 - k: Q_i = b_i ^ sum_k Q_(i-32+k) for the first 96
+// bytes, and the last 32 bytes (words 24-31) are what remains.  Every lag is
+// at least 4 bytes, so a word's four bytes are one step: a tap is a word of
+// the Q stream at that lag (one v_alignbyte when the lag is not a multiple
+// of 4), and the seven adjacent tap pairs come from a pair stream P2_i =
+// Q_(i-1) ^ Q_i at lag 31 - k.  About 14 VALU per word; then 8 one-word
+// chain steps: 24 lookups per segment instead of 100.  SKIP16: words 0-15
+// are zero in every lane (so is their part of Q).
+__device__ __forceinline__ uint32_t alignbyte(uint32_t hi, uint32_t lo, int s)
+{
+    return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)s);
+}
+
+template <bool SKIP16>
+__device__ __forceinline__ uint32_t tail_bytes8(const uint32_t (&R)[32], uint32_t tab_lds)
+{
+    uint32_t Q[24], P2[25];
+    // the word of stream W (Q or P2, zero outside [0, n)) at byte lag L from word j
+    auto lagw = [&](const uint32_t* W, int n, int j, int L) -> uint32_t {
+        const int q = L >> 2, s = L & 3;
+        const int hi = j - q, lo = j - q - 1;
+        const uint32_t h = (hi >= 0 && hi < n && !(SKIP16 && hi < 16)) ? W[hi] : 0u;
+        if (s == 0) {
+            return h;
+        }
+        const uint32_t l = (lo >= 0 && lo < n && !(SKIP16 && lo < 16)) ? W[lo] : 0u;
+        return alignbyte(h, l, 4 - s);
+    };
+    auto taps = [&](int j, int nq) -> uint32_t {
+        // singles k = 0, 6, 20 (lags 32, 26, 12); pairs k = 8, 10, 13, 18, 22,
+        // 25, 27 from P2 at lags 23, 21, 18, 13, 9, 6, 4
+        uint32_t t = xor3(lagw(Q, nq, j, 32), lagw(Q, nq, j, 26), lagw(Q, nq, j, 12));
+        t = xor3(t, lagw(P2, nq + 1, j, 23), lagw(P2, nq + 1, j, 21));
+        t = xor3(t, lagw(P2, nq + 1, j, 18), lagw(P2, nq + 1, j, 13));
+        t = xor3(t, lagw(P2, nq + 1, j, 9), lagw(P2, nq + 1, j, 6));
+        return t ^ lagw(P2, nq + 1, j, 4);
+    };
+#pragma unroll
+    for (int j = 0; j < 24; ++j) {
+        if (SKIP16 && j < 16) {
+            Q[j] = 0u;
+            P2[j] = 0u;
+            continue;
+        }
+        Q[j] = R[j] ^ taps(j, j);
+        P2[j] = Q[j] ^ alignbyte(Q[j], j > 0 ? Q[j - 1] : 0u, 3);
+    }
+    P2[24] = alignbyte(0u, Q[23], 3);  // Q_95 (Q_96 is not a quotient byte)
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 24; j < 32; ++j) {
+        c = step11(c, R[j] ^ taps(j, 24), tab_lds);
+    }
+    return c;
+}
+
 // Word w (0..31) of this lane's 128-byte line in an LDS slot (the pieces are
 // XOR-swizzled; rd_off is the lane's swizzled line base, see k_fold).
 __device__ __forceinline__ lds_u32* line_word(uint32_t slot, uint32_t rd_off, uint32_t w)
@@ -936,6 +996,13 @@ constexpr bool kSnakeRounds = BMQCRC_SNAKE != 0;
 #endif
 constexpr bool kTwoEnded = BMQCRC_TWO_ENDED != 0;
 
+#ifndef BMQCRC_BYTE_FOLD
+#define BMQCRC_BYTE_FOLD 1  // remainder words folded to 8 at byte granularity first (8-wave
+                            // blocks): 1 every group (product), 2 one-line groups only, 0
+                            // never: the 11-bit chains over all 32 words (A/B)
+#endif
+constexpr int kByteFold = BMQCRC_BYTE_FOLD;
+
 #ifndef BMQCRC_HORNER11
 #define BMQCRC_HORNER11 1  // 0: byte-sliced remainder tables in every block shape (round 4; A/B)
 #endif
@@ -982,9 +1049,15 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     const uint32_t wave_lds = tab_lds + kTab + wave * (kSlots * kSlotBytes);
     const uint32_t xb_lds = tab_lds + kTab + kLds;
     // a segment's raw CRC from its 32 remainder words (skip: words 0-15 are
-    // zero in every lane; a wave-uniform choice between two compiled copies)
-    auto remainder = [&](const uint32_t (&Rm)[32], bool skip) -> uint32_t {
-        if constexpr (H11) {
+    // zero in every lane; one_line: the group's streams are one line; both
+    // wave-uniform, choosing between compiled copies)
+    auto remainder = [&](const uint32_t (&Rm)[32], bool skip, bool one_line) -> uint32_t {
+        if constexpr (H11 && kByteFold != 0) {
+            if (kByteFold == 1 || one_line) {
+                return skip ? tail_bytes8<true>(Rm, tab_lds) : tail_bytes8<false>(Rm, tab_lds);
+            }
+            return tail_chains11(Rm, tab_lds);  // (skip is set for one-line groups only)
+        } else if constexpr (H11) {
             return skip ? tail_chains11<8>(Rm, tab_lds) : tail_chains11(Rm, tab_lds);
         } else {
             return skip ? tail_horner<8>(Rm, tab_lds) : tail_horner(Rm, tab_lds);
@@ -1508,7 +1581,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
                     issue_first_rounds(H);
                     uint32_t Rm[32];
                     fold_rounds(H, Rm);
-                    uint32_t x = contribution(H, remainder(Rm, false));
+                    uint32_t x = contribution(H, remainder(Rm, false, H.R == 1u));
 #pragma unroll
                     for (int o = 32; o > 0; o >>= 1) {
                         x ^= (uint32_t)__shfl_xor((int)x, o);
@@ -1604,7 +1677,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
                 }
                 finish(C, x);
             } else {
-                finish(C, remainder(Rm, C.hskip != 0u));
+                finish(C, remainder(Rm, C.hskip != 0u, C.R == 1u));
             }
         }
     } else {
@@ -1670,7 +1743,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
             ref2 = map_segment(a, &pl, s3, g3 < ngroups && s3 < total, identity, uni, sorted, ep);
             issue_first_rounds(G);
         }
-        finish(C, remainder(Rm, C.hskip != 0u));
+        finish(C, remainder(Rm, C.hskip != 0u, C.R == 1u));
         g = g1;
         g1 = g2;
         g2 = g3;

@@ -233,6 +233,60 @@ def test_chains11_match_horner():
         assert chains11(words) == horner_words(words)
 
 
+def bytes8(words, skip16=False):
+    """k_fold's tail_bytes8 (BMQCRC_BYTE_FOLD): the 32 remainder words folded
+    at byte granularity with the same taps (P(z) = 0 for z = x^8) to 8 words,
+    word-parallel with v_alignbyte windows and the pair stream, then 8
+    one-word chain steps."""
+    def alignbyte(hi, lo, s):
+        return (((hi << 32) | lo) >> (8 * s)) & 0xFFFFFFFF
+
+    Q = [0] * 24
+    P2 = [0] * 25
+
+    def lagw(W, n, j, L):
+        q, s = L >> 2, L & 3
+        hi, lo = j - q, j - q - 1
+        h = W[hi] if 0 <= hi < n and not (skip16 and hi < 16) else 0
+        if s == 0:
+            return h
+        lo_v = W[lo] if 0 <= lo < n and not (skip16 and lo < 16) else 0
+        return alignbyte(h, lo_v, 4 - s)
+
+    def taps(j, nq):
+        t = lagw(Q, nq, j, 32) ^ lagw(Q, nq, j, 26) ^ lagw(Q, nq, j, 12)
+        for L in (23, 21, 18, 13, 9, 6, 4):
+            t ^= lagw(P2, nq + 1, j, L)
+        return t
+
+    for j in range(24):
+        if skip16 and j < 16:
+            continue
+        Q[j] = words[j] ^ taps(j, j)
+        P2[j] = Q[j] ^ alignbyte(Q[j], Q[j - 1] if j > 0 else 0, 3)
+    P2[24] = alignbyte(0, Q[23], 3)
+    c = 0
+    for j in range(24, 32):
+        c = mul_y(c ^ words[j] ^ taps(j, 24))
+    return c
+
+
+def test_bytes8_match_horner():
+    # the byte-granular relation: same taps as the word ring
+    assert [k for k in G.min_poly_of_y() if k < 32] == TAPS
+    rng = np.random.default_rng(8)
+    for _ in range(200):
+        words = [int(w) for w in rng.integers(0, 2**32, size=32, dtype=np.uint64)]
+        assert bytes8(words) == horner_words(words)
+        zero_a = [0] * 16 + words[16:]
+        assert bytes8(zero_a, skip16=True) == bytes8(zero_a) == horner_words(zero_a)
+    for w in (1, 0x80000000, 0xFFFFFFFF, 0x000000FF, 0xFF000000):
+        for pos in (0, 5, 15, 16, 23, 24, 31):
+            words = [0] * 32
+            words[pos] = w
+            assert bytes8(words) == horner_words(words)
+
+
 def test_one_line_horner_skip():
     # One-line groups: the remainder is the line, and words before the lowest
     # S of the wave are zero, so hskip = min(sl) // 8 steps can be skipped.
