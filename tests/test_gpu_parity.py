@@ -724,6 +724,13 @@ def test_one_segment_pipeline_shapes(cuda, n):
     run(np.full(n, 256), "256 B contiguous", aligned=True, seeds=False)
     run(np.full(n, 64), "64 B contiguous", aligned=True)
     run(rng.integers(0, 129, size=n), "one line or two")
+    # streams of at most 64 bytes at any alignment: every group in its lines'
+    # second halves (half-line rounds, round 5), with byte cuts at both ends
+    # and seed words anywhere in the half
+    run(rng.integers(0, 50, size=n), "at most 49 B (half lines)")
+    run(rng.integers(0, 50, size=n), "at most 49 B, no seeds", seeds=False)
+    run(np.where(rng.integers(0, 8, size=n) == 0, 64, rng.integers(0, 50, size=n)),
+        "half lines with full-line groups between")
     past = rng.integers(0, 2049, size=n)
     past[rng.integers(0, n, size=max(1, n // 20000))] = rng.integers(2049, 100_000)
     run(past, "a few past the bound")

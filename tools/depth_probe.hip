@@ -12,6 +12,9 @@
 //   depth 1: k_fold's schedule (wait, read, issue the next group, work)
 //   depth 2: two groups in flight (wait for the older, read, issue the group
 //            after the next into the freed slot, work)
+//   depth 3: two ADJACENT groups issued together and waited for together
+//            (twice the contiguous bytes per wave request; the work doubled)
+//   depth 4: the same with the two groups half the batch apart
 // Shapes: 128-byte messages (every piece from HBM) and 64-byte messages
 // (pieces 0-3 from a zero line, or masked off).  Four 1 GiB regions are
 // cycled so that every launch reads HBM, not the Infinity Cache.
@@ -118,6 +121,34 @@ __global__ __launch_bounds__(512, 1) void probe(const uint8_t* base, uint64_t ng
         round_src((uint64_t)(uintptr_t)base + g * gbytes, msg_bytes, s);
         dma_round(slot, s, exec_mask);
     };
+    if (depth >= 3) {
+        // two groups issued together into both slots, waited for together,
+        // then the next pair: adjacent (depth 3: 8 KiB of 64-byte messages
+        // contiguous) or half the batch apart (depth 4)
+        const uint64_t half = ngroups / 2;
+        const uint64_t g0 = depth == 3 ? 2 * (blockIdx.x * wpb + wave) : blockIdx.x * wpb + wave;
+        const uint64_t gstep = depth == 3 ? 2 * stride : stride;
+        for (uint64_t g = g0; depth == 3 ? g + 1 < ngroups : g < half; g += gstep) {
+            issue(g, wl);
+            issue(depth == 3 ? g + 1 : g + half, wl + kSlotBytes);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            uint32_t x = 0;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+#pragma unroll
+                for (int kk = 0; kk < 8; ++kk) {
+                    const uint32_t off = h * kSlotBytes + lane * 128u + 16u * (uint32_t)kk;
+                    x ^= *(const __attribute__((address_space(3))) uint32_t*)(uintptr_t)(wl + off);
+                }
+            }
+            acc ^= x;
+            acc = fake_work(acc, 2 * work);
+        }
+        if (acc == 0x12345678u) {
+            sink[0] = acc;
+        }
+        return;
+    }
     uint64_t g = blockIdx.x * wpb + wave;
     if (g >= ngroups) {
         return;
@@ -180,8 +211,8 @@ int main()
     // launch region slice (4 launches cycle the four regions)
     for (const Shape& sh : shapes) {
         const uint64_t ngroups = (256ull << 20) / (64ull * sh.msg_bytes);
-        for (uint32_t depth : {1u, 2u}) {
-            for (uint32_t work : {0u, 200u, 400u, 800u}) {
+        for (uint32_t depth : {1u, 2u, 3u, 4u}) {
+            for (uint32_t work : {0u, 200u}) {
                 auto launch = [&](int r) {
                     hipLaunchKernelGGL(probe, dim3(cus), dim3(512), 0, 0, buf + (r % nreg) * region,
                                        ngroups, sh.msg_bytes, sh.masked, depth, work, sink);
