@@ -111,6 +111,11 @@ struct BatchArgs {
     // k_plan_sort instead of k_plan_map (the host does so for a while after
     // a map on this workspace was given up: the GPU is shared, kPairAfterVoid)
     uint32_t pair;
+    // set by the launcher: a batch of fewer groups than 4-wave blocks x CUs
+    // runs its groups one per block first (group k * gridDim.x + blockIdx.x
+    // for claim k) over every CU, instead of filling 4-wave blocks on a
+    // quarter of them
+    uint32_t spread;
 };
 
 // Ragged batches planned with the pair after k_fold reports a given-up map

@@ -130,6 +130,15 @@ __device__ __forceinline__ uint32_t gmul(uint32_t v, uint32_t w)
     return acc;
 }
 
+#ifndef BMQCRC_XB_FIRST
+#define BMQCRC_XB_FIRST 1  // 0: the move factor's product starts with byte 0's factor (A/B)
+#endif
+constexpr bool kXbFirst = BMQCRC_XB_FIRST != 0;
+#ifndef BMQCRC_SPREAD
+#define BMQCRC_SPREAD 1  // 0: small batches fill 4-wave blocks on fewer CUs (A/B)
+#endif
+constexpr bool kSpread = BMQCRC_SPREAD != 0;
+
 // v * x^(8 dist) mod P: the move of a CRC past dist zero bytes, as the
 // product of the factors of dist's bytes (tables XBYTES[i][b] = x^(8 b 256^i)
 // in LDS at xb): one lookup per byte position any lane needs and one 160-VALU
@@ -139,11 +148,28 @@ __device__ __forceinline__ uint32_t mul_xbytes(uint32_t v, uint32_t dist, uint32
     if (__ballot(dist != 0) == 0) {
         return v;
     }
-    uint32_t f = *(const lds_u32*)(uintptr_t)(xb + 4u * (dist & 0xffu));
+    // the first byte position any lane needs starts the product (a lane whose
+    // byte there is 0 looks up x^0 = 1): one 160-VALU multiply fewer than
+    // starting from byte 0, whose factor is 1 in every lane when the
+    // distances are multiples of 256 (uniform messages, segment moves)
+    if constexpr (!kXbFirst) {  // A/B: round 4's form
+        uint32_t f = *(const lds_u32*)(uintptr_t)(xb + 4u * (dist & 0xffu));
 #pragma unroll
-    for (int i = 1; i < 4; ++i) {
-        if (__ballot((dist >> (8 * i)) != 0) != 0) {
-            f = gmul(f, *(const lds_u32*)(uintptr_t)(xb + 1024u * i + 4u * ((dist >> (8 * i)) & 0xffu)));
+        for (int i = 1; i < 4; ++i) {
+            if (__ballot((dist >> (8 * i)) != 0) != 0) {
+                f = gmul(f, *(const lds_u32*)(uintptr_t)(xb + 1024u * i + 4u * ((dist >> (8 * i)) & 0xffu)));
+            }
+        }
+        return gmul(v, f);
+    }
+    uint32_t f = 0;
+    bool have = false;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (__ballot(((dist >> (8 * i)) & 0xffu) != 0) != 0) {
+            const uint32_t t = *(const lds_u32*)(uintptr_t)(xb + 1024u * i + 4u * ((dist >> (8 * i)) & 0xffu));
+            f = have ? gmul(f, t) : t;
+            have = true;
         }
     }
     return gmul(v, f);
@@ -1116,7 +1142,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     FOLD_STAMP(0)
     // the wave's first group (claim k = wave, see gid below), as if
     // segment = message
-    const uint32_t gfirst = blockIdx.x * WPB + wave;
+    const uint32_t gfirst = a.spread ? wave * gridDim.x + blockIdx.x : blockIdx.x * WPB + wave;
     const uint32_t sid = gfirst * 64u + (uint32_t)lane;
     const SegDesc spec = fetch_desc(a, SegRef{sid, 0u}, sid < a.n);
     // remainder-reduction tables -> LDS (8 KiB, once per block; no DMA in
@@ -1203,6 +1229,9 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     // 475-534 us, profiles/r04/fold_trace/).  gid grows with k.
     const uint32_t nbk = gridDim.x;
     auto gid = [&](uint32_t k) {
+        if (a.spread) {
+            return k * nbk + blockIdx.x;
+        }
         const uint32_t r = k / (uint32_t)WPB;
         const uint32_t b = (kSnakeRounds && !ONE && (r & 1u)) ? nbk - 1u - blockIdx.x : blockIdx.x;
         return (b + nbk * r) * (uint32_t)WPB + k % (uint32_t)WPB;
@@ -1217,7 +1246,9 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     // counts, and a claim is valid while they sum to less than K.
     const bool back = kTwoEnded && wave >= (uint32_t)WPB / 2u;
     uint32_t kb = 0;  // this block's claims (gid(k) < ngroups exactly for k < kb)
-    if (kTwoEnded) {
+    if (kTwoEnded && a.spread) {
+        kb = blockIdx.x < ngroups ? (ngroups - blockIdx.x - 1u) / nbk + 1u : 0u;
+    } else if (kTwoEnded) {
         const uint32_t full = ngroups / (nbk * (uint32_t)WPB);
         kb = full * (uint32_t)WPB;
         const uint32_t b = (kSnakeRounds && !ONE && (full & 1u)) ? nbk - 1u - blockIdx.x : blockIdx.x;
@@ -3031,23 +3062,30 @@ extern "C" int bmqcrc_launch_batch(const BatchArgs* a, void* stream, int num_cus
         (void)hipEventRecord((hipEvent_t)ev_start, s);
     }
     const bool one = a->spec == 1u && !a->whole && !(a->tune & 64u);
+    // few groups: one per block over every CU first (BatchArgs::spread)
+    BatchArgs b = *a;
+    b.spread = 0u;
+    if (kSpread && !wide && grid < cus && max_groups > grid) {
+        grid = std::min<uint64_t>(max_groups, cus);
+        b.spread = 1u;
+    }
     const dim3 gd((unsigned)grid), bd(wpb * 64u);
     if (a->tune & 1u) {  // A/B: default-policy LDS-DMA for long streams too
         if (wide) {
-            hipLaunchKernelGGL((k_fold<false, false, 8>), gd, bd, 0, s, *a);
+            hipLaunchKernelGGL((k_fold<false, false, 8>), gd, bd, 0, s, b);
         } else {
-            hipLaunchKernelGGL((k_fold<false, false, 4>), gd, bd, 0, s, *a);
+            hipLaunchKernelGGL((k_fold<false, false, 4>), gd, bd, 0, s, b);
         }
     } else if (one) {  // default: non-temporal LDS-DMA for long streams (once-read)
         if (wide) {
-            hipLaunchKernelGGL((k_fold<true, true, 8>), gd, bd, 0, s, *a);
+            hipLaunchKernelGGL((k_fold<true, true, 8>), gd, bd, 0, s, b);
         } else {
-            hipLaunchKernelGGL((k_fold<true, true, 4>), gd, bd, 0, s, *a);
+            hipLaunchKernelGGL((k_fold<true, true, 4>), gd, bd, 0, s, b);
         }
     } else if (wide) {
-        hipLaunchKernelGGL((k_fold<true, false, 8>), gd, bd, 0, s, *a);
+        hipLaunchKernelGGL((k_fold<true, false, 8>), gd, bd, 0, s, b);
     } else {
-        hipLaunchKernelGGL((k_fold<true, false, 4>), gd, bd, 0, s, *a);
+        hipLaunchKernelGGL((k_fold<true, false, 4>), gd, bd, 0, s, b);
     }
     if (ev_stop) {
         (void)hipEventRecord((hipEvent_t)ev_stop, s);

@@ -25,7 +25,9 @@ for v in base $VARIANTS; do
   if [ $v = base ]; then restore; else cp $lib/variant_$v.so $lib/libbmqcrc.so; fi
   for w in ${CONFIGS:-"1048576:256:4" "4194304:256:4" "2097152:128:4" "4194304:64:4" "1048576:200:4" "zipf_4M" "zipf_4M:0/8" "64k_x_64KiB"}; do
     IFS=: read -r a b c <<< "$w"
-    if [ -n "$c" ]; then
+    if [ -n "$c" ] && [ "$c" = 0 ]; then
+      args="--config 1M_x_256B --msgs $a --msg-bytes $b"; tag=${a}_${b}_resident
+    elif [ -n "$c" ]; then
       args="--config 1M_x_256B --msgs $a --msg-bytes $b --rotate $c"; tag=${a}_$b
     elif [ -n "$b" ]; then
       args="--config $a --shard $b"; tag=${a}_shard
@@ -33,7 +35,7 @@ for v in base $VARIANTS; do
       args="--config $a"; tag=$a
     fi
     rc=0
-    line=$(timeout -k 10 240 python bench.py $args --steps 30 --warmup 5 --no-cpu-baseline \
+    line=$(timeout -k 10 240 python bench.py $args --steps ${STEPS:-30} --warmup 5 --no-cpu-baseline \
         2> $out/${v}_$tag.err | tail -1) || rc=$?
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then restore; echo "bench rc $rc ($v $tag)"; exit $rc; fi
     echo "{\"variant\": \"$v\", \"round\": $r, \"args\": \"$args\", \"bench\": $line}" >> $res
