@@ -485,7 +485,18 @@ __device__ __forceinline__ uint32_t alignbyte(uint32_t hi, uint32_t lo, int s)
     return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)s);
 }
 
-template <bool SKIP16>
+// One word per step with the byte-sliced "times y" tables (tab[k][b], k < 4:
+// 4-wave blocks' 8 KiB tables, tail_horner's), four lookups.
+__device__ __forceinline__ uint32_t step8(uint32_t c, uint32_t r, uint32_t tab_lds)
+{
+    const uint32_t v = c ^ r;
+    return xor3(tab_lookup(tab_lds, 0, v & 0xffu), tab_lookup(tab_lds, 1, (v >> 8) & 0xffu),
+                tab_lookup(tab_lds, 2, (v >> 16) & 0xffu)) ^
+           tab_lookup(tab_lds, 3, v >> 24);
+}
+
+// BYTE_TABLES: the last 8 steps with the byte-sliced tables (4-wave blocks).
+template <bool SKIP16, bool BYTE_TABLES = false>
 __device__ __forceinline__ uint32_t tail_bytes8(const uint32_t (&R)[32], uint32_t tab_lds)
 {
     uint32_t Q[24], P2[25];
@@ -523,7 +534,8 @@ __device__ __forceinline__ uint32_t tail_bytes8(const uint32_t (&R)[32], uint32_
     uint32_t c = 0;
 #pragma unroll
     for (int j = 24; j < 32; ++j) {
-        c = step11(c, R[j] ^ taps(j, 24), tab_lds);
+        c = BYTE_TABLES ? step8(c, R[j] ^ taps(j, 24), tab_lds)
+                        : step11(c, R[j] ^ taps(j, 24), tab_lds);
     }
     return c;
 }
@@ -1028,6 +1040,10 @@ constexpr bool kTwoEnded = BMQCRC_TWO_ENDED != 0;
                             // never: the 11-bit chains over all 32 words (A/B)
 #endif
 constexpr int kByteFold = BMQCRC_BYTE_FOLD;
+#ifndef BMQCRC_BYTE_FOLD4
+#define BMQCRC_BYTE_FOLD4 1  // 0: 4-wave blocks keep the two-word Horner over all 32 words (A/B)
+#endif
+constexpr bool kByteFold4 = BMQCRC_BYTE_FOLD4 != 0;
 
 #ifndef BMQCRC_HORNER11
 #define BMQCRC_HORNER11 1  // 0: byte-sliced remainder tables in every block shape (round 4; A/B)
@@ -1085,6 +1101,10 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
             return tail_chains11(Rm, tab_lds);  // (skip is set for one-line groups only)
         } else if constexpr (H11) {
             return skip ? tail_chains11<8>(Rm, tab_lds) : tail_chains11(Rm, tab_lds);
+        } else if constexpr (kByteFold4) {
+            // 4-wave blocks: the byte fold too, its last 8 steps on the byte
+            // tables (32 lookups per segment instead of 128)
+            return skip ? tail_bytes8<true, true>(Rm, tab_lds) : tail_bytes8<false, true>(Rm, tab_lds);
         } else {
             return skip ? tail_horner<8>(Rm, tab_lds) : tail_horner(Rm, tab_lds);
         }
