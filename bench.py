@@ -118,12 +118,14 @@ def parse():
                    help="end-to-end mode: H2D from pinned host + CRC + D2H (for DESIGN.md)")
     p.add_argument("--no-strong-scaling", action="store_true",
                    help="N > 1: skip the strong-scaled Zipf object")
-    p.add_argument("--rotate", type=int, default=1,
+    p.add_argument("--rotate", type=int, default=None,
                    help="N > 1: every step (settle, warmup, timed, planned, declared, kernel "
                         "timing) takes the next of N copies of the batch (arena, offsets, "
                         "lengths, out), so a batch smaller than the 256 MiB Infinity Cache is "
-                        "read from HBM rather than replayed from the cache (configs[1]: "
-                        "--rotate 4 cycles 1.1 GiB)")
+                        "read from HBM rather than replayed from the cache.  Default: 4 for "
+                        "1M_x_256B (configs[1], 272 MiB: 4 copies cycle 1.1 GiB, so its line "
+                        "is an HBM figure; --rotate 1 replays one copy from the cache), 1 "
+                        "otherwise")
     p.add_argument("--plan-wait-us", type=int, default=None,
                    help="bmqcrc_plan_wait limit for this run (default: the library's 100 us; "
                         "0 gives every ragged batch's size-class map up: the fallback's cost)")
@@ -132,6 +134,8 @@ def parse():
                         "world as rank 0 sees it, without touching a GPU")
     a = p.parse_args()
     a.config_given = a.config is not None
+    if a.rotate is None:
+        a.rotate = 4 if a.config == "1M_x_256B" else 1
     if a.config is None:
         a.config = "64k_x_64KiB"
     return a
@@ -518,7 +522,9 @@ def pmc_traffic(config):
     summary of this config (profiles/rNN/<config>_summary.json): read =
     2 x FETCH_SIZE (gfx950 correction) + WRITE_SIZE, per MI355X_MICROARCH.md."""
     import glob
-    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", config + "_summary.json")))
+    # newest round first, and within a round its final/ set after the rest
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", config + "_summary.json")) +
+                   glob.glob(os.path.join(ROOT, "profiles", "r*", "final", config + "_summary.json")))
     if not paths:
         return None, None
     with open(paths[-1]) as f:
