@@ -1045,6 +1045,19 @@ constexpr int kByteFold = BMQCRC_BYTE_FOLD;
 #endif
 constexpr bool kByteFold4 = BMQCRC_BYTE_FOLD4 != 0;
 
+#ifndef BMQCRC_ONE_PRIO
+#define BMQCRC_ONE_PRIO 2  // the one-segment kernel's wave behind its SIMD partner in groups
+                           // takes issue priority: 2 in groups of two or more lines (product),
+                           // 1 in every group, 0 never (A/B)
+#endif
+constexpr int kOnePrio = BMQCRC_ONE_PRIO;
+
+#ifndef BMQCRC_ONE_CLAIMS
+#define BMQCRC_ONE_CLAIMS 0  // 1: the one-segment kernel claims its groups from the block's LDS
+                             // counter too (the claiming loop and block list; A/B)
+#endif
+constexpr bool kOneClaims = BMQCRC_ONE_CLAIMS != 0;
+
 #ifndef BMQCRC_HORNER11
 #define BMQCRC_HORNER11 1  // 0: byte-sliced remainder tables in every block shape (round 4; A/B)
 #endif
@@ -1084,6 +1097,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     __shared__ uint32_t claim_ctr, long_n;
     __shared__ unsigned long long claim2;  // two-ended claims: front count | back count << 32
     __shared__ uint32_t long_list[kLongListCap];
+    __shared__ uint32_t one_prog[WPB];  // BMQCRC_ONE_PRIO: groups each wave has started
 
     const int lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1109,6 +1123,9 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
             return skip ? tail_horner<8>(Rm, tab_lds) : tail_horner(Rm, tab_lds);
         }
     };
+    if (threadIdx.x < (uint32_t)WPB) {
+        one_prog[threadIdx.x] = 0u;
+    }
     if (threadIdx.x == 0) {
         claim_ctr = WPB;
         claim2 = 0ull;
@@ -1390,7 +1407,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
             // the wave's second pass (below); with u = 1 an empty message is
             // folded whole (its seed)
             const bool ok = spec_u == 1u ? nseg <= 1u : nseg == spec_u;
-            if constexpr (ONE) {
+            if constexpr (ONE && !kOneClaims) {
                 long_seen |= __ballot(valid && !ok) != 0;
             } else if (__ballot(valid && !ok) != 0 && lane == 0) {  // group gg on the block's list
                 const uint32_t at = atomicAdd(&long_n, 1u);
@@ -1607,7 +1624,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
         const uint32_t mpg = 64u / spec_u;  // messages per group
         const bool listed = nlong <= kLongListCap;
         for (uint32_t j = wave;; j += WPB) {
-            const uint32_t gg = ONE ? gfirst + (j / (uint32_t)WPB) * nbk * (uint32_t)WPB
+            const uint32_t gg = (ONE && !kOneClaims) ? gfirst + (j / (uint32_t)WPB) * nbk * (uint32_t)WPB
                                 : listed ? (j < nlong ? long_list[j] : ngroups) : gid(j);
             if (gg >= ngroups) {
                 break;
@@ -1661,7 +1678,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     Group G;
     SegDesc nxt = {0ull, 0u, 0u, 0u, 0u};
     SegRef ref2 = {0u, 0u};
-    if constexpr (ONE) {
+    if constexpr (ONE && !kOneClaims) {
         // The speculative one-segment kernel: every group the same work, so
         // wave w of block b keeps round 3's static share, groups
         // g0 + j stride (the set its claims k = w, w + WPB, ... name, gid
@@ -1697,7 +1714,32 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
             FOLD_STAMP(2)
         }
         [[maybe_unused]] bool first = true;
+        [[maybe_unused]] uint32_t it = 0;
         for (; g < ngroups; g += stride) {
+            if constexpr (kOnePrio != 0) {
+                // The two waves of a SIMD (w and w ^ WPB/2) take the same
+                // number of groups, but the older one wins every issue tie:
+                // per-wave stamps put the younger four waves of every block
+                // 16 % behind at the end (1M x 256 B: 57.6 against 49.5 us,
+                // profiles/r05/probe/fold_trace_one_raw.txt), the SIMD then
+                // left to one wave.  The one behind in groups raises its
+                // priority until even (groups of two or more lines: for one-line
+                // groups the exchange costs more than the balance gains).
+                // Same box, HBM-resident: 2M x 256 B +3.9 %, 4M x 256 B +2 %,
+                // the rest unchanged (profiles/r05/ab/one_prio_ab.jsonl).
+                if (kOnePrio == 1 || G.R >= 2u) {
+                    if (lane == 0) {
+                        one_prog[wave] = it;
+                    }
+                    const uint32_t other = one_prog[wave ^ ((uint32_t)WPB / 2u)];
+                    if (it > other) {
+                        __builtin_amdgcn_s_setprio(0);
+                    } else {
+                        __builtin_amdgcn_s_setprio(1);
+                    }
+                    ++it;
+                }
+            }
             uint32_t Rm[32];
             fold_rounds(G, Rm);
 #if BMQCRC_FOLD_DIAG
@@ -1801,7 +1843,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     }
     }
     FOLD_STAMP(5)
-    if constexpr (ONE) {
+    if constexpr (ONE && !kOneClaims) {
         if (long_seen) {
             second_pass(0u);
         }
