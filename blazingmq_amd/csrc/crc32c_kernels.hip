@@ -1716,7 +1716,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
         [[maybe_unused]] bool first = true;
         [[maybe_unused]] uint32_t it = 0;
         for (; g < ngroups; g += stride) {
-            if constexpr (kOnePrio != 0) {
+            if constexpr (kOnePrio != 0 && WPB == 8) {
                 // The two waves of a SIMD (w and w ^ WPB/2) take the same
                 // number of groups, but the older one wins every issue tie:
                 // per-wave stamps put the younger four waves of every block
@@ -1727,6 +1727,8 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
                 // groups the exchange costs more than the balance gains).
                 // Same box, HBM-resident: 2M x 256 B +3.9 %, 4M x 256 B +2 %,
                 // the rest unchanged (profiles/r05/ab/one_prio_ab.jsonl).
+                // 8-wave blocks only: a 4-wave block's partner wave is in
+                // another block (two per CU) or absent (one per CU).
                 if (kOnePrio == 1 || G.R >= 2u) {
                     if (lane == 0) {
                         one_prog[wave] = it;
