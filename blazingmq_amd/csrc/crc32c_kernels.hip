@@ -1554,7 +1554,29 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
         }
         return contrib;
     };
-    auto finish = [&](const Group& C, uint32_t crc) {
+    // A group's result: per lane nothing, a store or an XOR-atomic into
+    // out[msg].  finish computes it; commit issues it one group later, after
+    // the group after it has issued its loads (round 5).  A store issued
+    // just before a wave's next s_waitcnt vmcnt is waited for there too
+    // (stores share the load counter on gfx950), so its acknowledgement
+    // latency sat on every group's critical path: a diagnostic build without
+    // the stores ran 4M x 256 B 9 %, 64- and 128-byte messages 15 % faster.
+    // Committed after the next group's loads are issued, same box: 2M x
+    // 128 B +12 %, 4M x 64 B +9 %, 200 B +5 %, 4M x 256 B +2 %; committed
+    // right after the wait instead, 64 B lost 5 % (the store then delays
+    // the next loads) (profiles/r05/ab/deferred_commit_ab.jsonl).
+    struct Pending {
+        uint32_t msg, val, mode;  // mode: 0 none, 1 store, 2 atomic XOR
+    };
+    auto commit = [&](const Pending& P) {
+        if (P.mode == 1u) {
+            a.out[P.msg] = P.val;
+        } else if (P.mode == 2u) {
+            atomicXor(&a.out[P.msg], P.val);
+        }
+    };
+    auto finish = [&](const Group& C, uint32_t crc) -> Pending {
+        Pending P = {C.msg, 0u, 0u};
         if (ONE) {
             // every segment is a whole message ending at E: un-shift the
             // padding, invert, store
@@ -1563,10 +1585,9 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
             if (__ballot(padE != 0) != 0 && C.valid) {
                 contrib = gmul(crc, xneg8[padE]);
             }
-            if (C.valid) {
-                a.out[C.msg] = contrib ^ 0xffffffffu;
-            }
-            return;
+            P.val = contrib ^ 0xffffffffu;
+            P.mode = C.valid ? 1u : 0u;
+            return P;
         }
         uint32_t contrib = contribution(C, crc);
         // XOR-reduce each run of adjacent lanes holding the same message, then
@@ -1577,10 +1598,9 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
         // a head stores plainly only when its run is the whole message.
         if (__ballot(C.valid && C.nseg != 1u) == 0) {
             // every segment of this group is a whole message: no runs to combine
-            if (C.valid) {
-                a.out[C.msg] = contrib;
-            }
-            return;
+            P.val = contrib;
+            P.mode = C.valid ? 1u : 0u;
+            return P;
         }
         const uint32_t key = C.valid ? C.msg : 0xffffffffu;
         const uint32_t pkey = (uint32_t)__shfl_up((int)key, 1);
@@ -1596,13 +1616,12 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
                 contrib ^= ov;
             }
         }
+        P.val = contrib;
         if (C.valid && head) {
-            if (C.k == 0 && rend - (uint32_t)lane == C.nseg) {
-                a.out[C.msg] = contrib;  // the whole message is this run
-            } else {
-                atomicXor(&a.out[C.msg], contrib);
-            }
+            // a plain store when the whole message is this run
+            P.mode = (C.k == 0 && rend - (uint32_t)lane == C.nseg) ? 1u : 2u;
         }
+        return P;
     };
 
     // Speculative launches only: the block's messages of another segment
@@ -1715,6 +1734,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
         }
         [[maybe_unused]] bool first = true;
         [[maybe_unused]] uint32_t it = 0;
+        Pending pend = {0u, 0u, 0u};
         for (; g < ngroups; g += stride) {
             if constexpr (kOnePrio != 0 && WPB == 8) {
                 // The two waves of a SIMD (w and w ^ WPB/2) take the same
@@ -1764,17 +1784,20 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
                                    uni, sorted, ep);
                 issue_first_rounds(G);
             }
+            // the previous group's results, after the next group's loads
+            commit(pend);
             if (BMQCRC_ONE_DIAG & 1) {  // diagnostic: no remainder step (wrong CRCs)
                 uint32_t x = 0;
 #pragma unroll
                 for (int d = 0; d < 32; ++d) {
                     x ^= Rm[d];
                 }
-                finish(C, x);
+                pend = finish(C, x);
             } else {
-                finish(C, remainder(Rm, C.hskip != 0u, C.R == 1u));
+                pend = finish(C, remainder(Rm, C.hskip != 0u, C.R == 1u));
             }
         }
+        commit(pend);
     } else {
     uint32_t g = kTwoEnded ? claim() : gid(wave), g1 = ngroups, g2 = ngroups;  // (= gfirst)
     if (g < ngroups) {
@@ -1807,6 +1830,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
         FOLD_STAMP(2)
     }
     bool first_group = true;
+    Pending pend = {0u, 0u, 0u};
     while (g < ngroups) {
         // the claim of the group after g2, issued before this group's fold
         // (whose LDS reads cover the atomic's latency), taken below
@@ -1838,11 +1862,13 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
             ref2 = map_segment(a, &pl, s3, g3 < ngroups && s3 < total, identity, uni, sorted, ep);
             issue_first_rounds(G);
         }
-        finish(C, remainder(Rm, C.hskip != 0u, C.R == 1u));
+        commit(pend);  // the previous group's results, after the next group's loads
+        pend = finish(C, remainder(Rm, C.hskip != 0u, C.R == 1u));
         g = g1;
         g1 = g2;
         g2 = g3;
     }
+    commit(pend);
     }
     FOLD_STAMP(5)
     if constexpr (ONE && !kOneClaims) {
