@@ -1045,6 +1045,11 @@ constexpr int kByteFold = BMQCRC_BYTE_FOLD;
 #endif
 constexpr bool kByteFold4 = BMQCRC_BYTE_FOLD4 != 0;
 
+#ifndef BMQCRC_NT_RESULTS
+#define BMQCRC_NT_RESULTS 0  // 1: result stores with the non-temporal hint (A/B)
+#endif
+constexpr bool kNtResults = BMQCRC_NT_RESULTS != 0;
+
 #ifndef BMQCRC_ONE_PRIO
 #define BMQCRC_ONE_PRIO 2  // the one-segment kernel's wave behind its SIMD partner in groups
                            // takes issue priority: 2 in groups of two or more lines (product),
@@ -1570,7 +1575,11 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     };
     auto commit = [&](const Pending& P) {
         if (P.mode == 1u) {
-            a.out[P.msg] = P.val;
+            if (kNtResults) {
+                __builtin_nontemporal_store(P.val, &a.out[P.msg]);
+            } else {
+                a.out[P.msg] = P.val;
+            }
         } else if (P.mode == 2u) {
             atomicXor(&a.out[P.msg], P.val);
         }
