@@ -2405,7 +2405,8 @@ constexpr uint32_t kMapRegTiles = BMQCRC_MAP_REG_TILES;  // tiles kept in regist
 #ifndef BMQCRC_PLAN_SKIP
 #define BMQCRC_PLAN_SKIP 0  // timing diagnostics with the map voided (wrong maps, exact CRCs):
                             // 1 no histogram atomics, 2 no last-segment claims, 4 no full-run
-                            // writes, 8 no last-segment stores
+                            // writes, 8 no last-segment stores, 16 no long-run writes, 32 no
+                            // short-run writes, 64 full-run slots mapped but not stored
 #endif
 #ifndef BMQCRC_PLAN_FLAGS
 #define BMQCRC_PLAN_FLAGS 0  // 1: round 3's separate arrival flags (A/B)
@@ -2856,7 +2857,7 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
 #if BMQCRC_PLAN_DIAG != 4 && !(BMQCRC_PLAN_SKIP & 4)
             const uint32_t w = threadIdx.x >> 6;
             const uint64_t wbase = base + (uint64_t)(threadIdx.x & ~63u) * kPlanV;
-            if (ts) {
+            if (ts && !(BMQCRC_PLAN_SKIP & 32)) {
                 uint32_t e = xs - ns_all, ends[kPlanV];
 #pragma unroll
                 for (uint32_t v = 0; v < kPlanV; ++v) {
@@ -2871,13 +2872,22 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
                         q += sruns[w][q + st - 1u] <= j ? st : 0u;
                     }
                     const uint32_t k = j - (q ? sruns[w][q - 1u] : 0u);
+#if BMQCRC_PLAN_SKIP & 64
+                    if (k == 0xfffffff0u) {  // never: keeps the slot's search live
+                        a.firstk[0] = q;
+                    }
+#else
                     put_full(a, pos + j, (uint32_t)(wbase + q), k);
+#endif
                 }
             }
             uint64_t longs = 0;
 #pragma unroll
             for (uint32_t v = 0; v < kPlanV; ++v) {
                 longs |= __ballot(nf[v] > kMapShortRun);
+            }
+            if (BMQCRC_PLAN_SKIP & 16) {
+                longs = 0;
             }
             const uint32_t lpos = pos + ts + (xl - nl_all);
             for (; longs; longs &= longs - 1ull) {
@@ -2895,17 +2905,17 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
                         const uint32_t gf = (at2 + 63u) >> 6, ge = (at2 + n) >> 6;
                         const uint32_t kh = kGroupDesc && gf < ge ? 64u * gf - at2 : n;
                         const uint32_t kt = kGroupDesc && gf < ge ? 64u * ge - at2 : n;
-                        for (uint32_t k = (uint32_t)lane; k < kh; k += 64u) {
+                        for (uint32_t k = (uint32_t)lane; k < kh && !(BMQCRC_PLAN_SKIP & 64); k += 64u) {
                             put_full(a, at2 + k, i, k);
                         }
-                        if (kGroupDesc) {
+                        if (kGroupDesc && !(BMQCRC_PLAN_SKIP & 64)) {
                             const unsigned long long tag = (unsigned long long)ep << 32 | i;
                             for (uint32_t g = gf + (uint32_t)lane; g < ge; g += 64u) {
                                 a.gdesc[g] = tag;
                                 a.firstk[g] = 64u * g - at2;
                             }
                         }
-                        for (uint32_t k = kt + (uint32_t)lane; k < n; k += 64u) {
+                        for (uint32_t k = kt + (uint32_t)lane; k < n && !(BMQCRC_PLAN_SKIP & 64); k += 64u) {
                             put_full(a, at2 + k, i, k);
                         }
                         at2 += n;
