@@ -195,7 +195,9 @@ __device__ __forceinline__ uint32_t dpp_max(uint32_t v)
                                                         false));
 }
 
-__device__ __forceinline__ uint32_t wave_max(uint32_t v)
+// (the same steps leave lane l with the maximum of lanes 0..l: an inclusive
+// max-scan)
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v)
 {
     v = dpp_max<0x111, 0xf>(v);  // row_shr:1
     v = dpp_max<0x112, 0xf>(v);  // row_shr:2
@@ -203,7 +205,12 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v)
     v = dpp_max<0x118, 0xf>(v);  // row_shr:8
     v = dpp_max<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
     v = dpp_max<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max(v), 63);
 }
 
 // Inclusive prefix sum over the wave's 64 lanes by DPP (all lanes active):
@@ -2411,6 +2418,9 @@ constexpr uint32_t kMapRegTiles = BMQCRC_MAP_REG_TILES;  // tiles kept in regist
 #ifndef BMQCRC_PLAN_FLAGS
 #define BMQCRC_PLAN_FLAGS 0  // 1: round 3's separate arrival flags (A/B)
 #endif
+#ifndef BMQCRC_LONG_FLAT
+#define BMQCRC_LONG_FLAT 1  // long runs' entries and descriptors: 1 flattened over the wave, 0 run by run
+#endif
 #ifndef BMQCRC_PLAN_DIAG
 #define BMQCRC_PLAN_DIAG 0  // 3: per-block phase stamps, 4: the same without seginfo stores,
                             // 6: every block's first read of the exchanged words is stale
@@ -2449,6 +2459,10 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
     __shared__ uint32_t go;
     __shared__ PlanTail tail;
     __shared__ uint32_t sruns[kPlanBlock / 64][64 * kPlanV];  // per wave: short-run ends
+#if BMQCRC_LONG_FLAT
+    __shared__ uint32_t slong[kPlanBlock / 64][2][64 * kPlanV];  // per wave: long runs' starts, lengths
+    __shared__ uint32_t smark[kPlanBlock / 64][64];             // per wave: item-run starts in a chunk
+#endif
     const uint32_t nb = a.nblocks, ep = launch_epoch(a), bid = blockIdx.x;
     load_tail(a, min((uint64_t)bid * a.per_msg + a.per_msg, a.n), true, &tail);
     // epoch-tagged words the blocks exchange (plan_sync after the flags),
@@ -2890,6 +2904,84 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
                 longs = 0;
             }
             const uint32_t lpos = pos + ts + (xl - nl_all);
+#if BMQCRC_LONG_FLAT
+            if (longs) {
+                // Every long run of the wave at once: its head and tail
+                // entries (the partial groups at either end) are one list of
+                // items over the wave, its whole groups another, each walked
+                // 64 items per store.  (Run by run, a wave issued two to four
+                // partly filled stores per run, and the long runs' stores
+                // were 5.3 of the 1/8 shard's 21.5 us planner,
+                // profiles/r05/ab/planner/phase_stamps_fullrun_split.jsonl.)
+                // An item finds its run by a mark at the run's first item and
+                // a max-scan over the wave (run indices grow with their
+                // items); a wave's LDS operations complete in order, so
+                // marks, reads and clearing need no barrier.
+                uint32_t atv[kPlanV], nv[kPlanV], ni[kPlanV], ng[kPlanV];
+                uint32_t p = lpos;
+#pragma unroll
+                for (uint32_t v = 0; v < kPlanV; ++v) {
+                    const uint32_t n = nf[v] > kMapShortRun ? nf[v] : 0u;
+                    const uint32_t gf = (p + 63u) >> 6, ge = (p + n) >> 6;
+                    const bool whole = kGroupDesc && gf < ge;
+                    atv[v] = p;
+                    nv[v] = n;
+                    ni[v] = whole ? (64u * gf - p) + (p + n - 64u * ge) : n;
+                    ng[v] = whole ? ge - gf : 0u;
+                    p += n;
+                }
+                *(u32x4*)&slong[w][0][lane * kPlanV] = u32x4{atv[0], atv[1], atv[2], atv[3]};
+                *(u32x4*)&slong[w][1][lane * kPlanV] = u32x4{nv[0], nv[1], nv[2], nv[3]};
+                auto flat = [&](const uint32_t (&cnt)[kPlanV], auto&& body) {
+                    const uint32_t mine = cnt[0] + cnt[1] + cnt[2] + cnt[3];
+                    const uint32_t x = wave_incl_scan(mine);
+                    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+                    uint32_t s0 = x - mine, st[kPlanV];
+#pragma unroll
+                    for (uint32_t v = 0; v < kPlanV; ++v) {
+                        st[v] = cnt[v] ? s0 : 0xffffffffu;
+                        s0 += cnt[v];
+                    }
+                    *(u32x4*)&sruns[w][lane * kPlanV] = u32x4{st[0], st[1], st[2], st[3]};
+                    smark[w][lane] = 0u;
+                    uint32_t open = 0u;
+                    for (uint32_t j0 = 0; j0 < total; j0 += 64u) {
+#pragma unroll
+                        for (uint32_t v = 0; v < kPlanV; ++v) {
+                            if (st[v] - j0 < 64u) {
+                                smark[w][st[v] - j0] = (uint32_t)lane * kPlanV + v + 1u;
+                            }
+                        }
+                        uint32_t o = smark[w][lane];
+                        smark[w][lane] = 0u;
+                        o = max(wave_incl_max(o), open);
+                        open = (uint32_t)__builtin_amdgcn_readlane((int)o, 63);
+                        const uint32_t j = j0 + (uint32_t)lane;
+                        if (j < total) {
+                            const uint32_t q = o - 1u;  // o >= 1: a run's items start at 0
+                            body(q, j - sruns[w][q]);
+                        }
+                    }
+                };
+                if (!(BMQCRC_PLAN_SKIP & 64)) {
+                    flat(ni, [&](uint32_t q, uint32_t e) {
+                        const uint32_t at = slong[w][0][q], n = slong[w][1][q];
+                        const uint32_t gf = (at + 63u) >> 6, ge = (at + n) >> 6;
+                        const uint32_t h = kGroupDesc && gf < ge ? 64u * gf - at : n;
+                        const uint32_t slot = e < h ? at + e : 64u * ge + (e - h);
+                        put_full(a, slot, (uint32_t)(wbase + q), slot - at);
+                    });
+                    if (kGroupDesc) {
+                        flat(ng, [&](uint32_t q, uint32_t e) {
+                            const uint32_t at = slong[w][0][q];
+                            const uint32_t g = ((at + 63u) >> 6) + e;
+                            a.gdesc[g] = (unsigned long long)ep << 32 | (uint32_t)(wbase + q);
+                            a.firstk[g] = 64u * g - at;
+                        });
+                    }
+                }
+            }
+#else
             for (; longs; longs &= longs - 1ull) {
                 const int src = __builtin_ctzll(longs);
                 uint32_t at2 = (uint32_t)__builtin_amdgcn_readlane((int)lpos, src);
@@ -2922,6 +3014,7 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
                     }
                 }
             }
+#endif
 #endif
         }
         // last (or only) segments: one returning LDS atomic per message

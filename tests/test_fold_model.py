@@ -625,3 +625,86 @@ def test_claims_cover_every_group_once(ngroups, nbk, wpb):
                 break
             seen.append(g)
     assert sorted(seen) == list(range(ngroups))
+
+
+def _long_runs_flat(nf, lpos, short=16):
+    """k_plan_map's flattened long-run writes (BMQCRC_LONG_FLAT,
+    crc32c_kernels.hip phase 2): runs of more than `short` full segments laid
+    out from lpos in (lane, v) order; head and tail entries (the partial
+    groups at either end) as one item list, whole groups as another, each
+    walked 64 items at a time with a mark at each run's first item and an
+    inclusive max-scan.  Returns ({slot: (run, k)}, {group: (run, firstk)})."""
+    runs, p = [], lpos
+    for x in nf:
+        n = x if x > short else 0
+        gf, ge = (p + 63) >> 6, (p + n) >> 6
+        whole = gf < ge
+        ni = (64 * gf - p) + (p + n - 64 * ge) if whole else n
+        runs.append((p, n, ni, ge - gf if whole else 0))
+        p += n
+
+    def flat(counts, body):
+        starts, s = [], 0
+        for c in counts:
+            starts.append(s if c else None)
+            s += c
+        total, open_ = s, 0
+        for j0 in range(0, total, 64):
+            mark = [0] * 64
+            for q, st in enumerate(starts):
+                if st is not None and 0 <= st - j0 < 64:
+                    mark[st - j0] = q + 1
+            scan = np.maximum.accumulate(mark).tolist()
+            for lane in range(64):
+                o = max(scan[lane], open_)
+                if j0 + lane < total:
+                    q = o - 1
+                    body(q, j0 + lane - starts[q])
+            open_ = max(scan[63], open_)
+
+    ent, grp = {}, {}
+
+    def put_entry(q, e):
+        at, n = runs[q][0], runs[q][1]
+        gf, ge = (at + 63) >> 6, (at + n) >> 6
+        h = 64 * gf - at if gf < ge else n
+        slot = at + e if e < h else 64 * ge + (e - h)
+        assert slot not in ent
+        ent[slot] = (q, slot - at)
+
+    def put_group(q, e):
+        at = runs[q][0]
+        g = ((at + 63) >> 6) + e
+        assert g not in grp
+        grp[g] = (q, 64 * g - at)
+
+    flat([r[2] for r in runs], put_entry)
+    flat([r[3] for r in runs], put_group)
+    return ent, grp
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_long_runs_flat_cover_every_segment(seed):
+    """Every full segment of every long run is written exactly once: as an
+    entry (message, k) at its slot, or inside a whole group described by one
+    descriptor whose firstk is the group's first k -- against a brute-force
+    expansion; runs aligned to groups (no entries), runs inside one group and
+    runs spanning many."""
+    rng = np.random.default_rng(seed)
+    nf = rng.choice([0, 3, 17, 40, 63, 64, 65, 128, 200, 1000], size=256).tolist()
+    lpos = int(rng.integers(0, 64)) if seed else 0
+    if seed == 1:
+        nf = [64] * 256                                   # every run group-aligned
+    ent, grp = _long_runs_flat(nf, lpos)
+    want, p = {}, lpos
+    for q, x in enumerate(nf):
+        if x > 16:
+            for k in range(x):
+                want[p + k] = (q, k)
+            p += x
+    got = dict(ent)
+    for g, (q, k0) in grp.items():
+        for lane in range(64):
+            assert 64 * g + lane not in got
+            got[64 * g + lane] = (q, k0 + lane)
+    assert got == want
