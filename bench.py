@@ -169,13 +169,28 @@ REF_PUBLISHED_NS = {256: (30, "bmqp_crc32c.h:116"), 1024: (45, "bmqp_crc32c.h:11
                     1 << 20: (50937, "bmqp_crc32c.h:129")}
 
 
-def cpu_baseline(lens_np, seed, seconds):
+def gpu_numa_node(device):
+    """NUMA node of the GPU `device` (torch ordinal) from its PCI address,
+    or None."""
+    try:
+        import torch
+        p = torch.cuda.get_device_properties(device)
+        addr = "%04x:%02x:%02x.0" % (p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
+        with open("/sys/bus/pci/devices/%s/numa_node" % addr) as f:
+            node = int(f.read().strip())
+        return node if node >= 0 else None
+    except Exception:
+        return None
+
+
+def cpu_baseline(lens_np, seed, seconds, device=0):
     """Reference-equivalent CPU CRC32C (oracle, SSE4.2 3-way; BDE 4.39 is not
     available offline) on a bounded sample (first ~256 MiB of messages) of the
     same synthetic workload.  Three legs, each warm (one untimed pass) and
-    timed for >= 0.5 s: the batch on one thread, the batch on this GPU's share
-    of the host's threads (created once, before the clock; the test5 pattern,
-    one thread per byte-balanced message slice), and the reference's own
+    timed for >= 0.3 s: the batch on one thread, the batch on this GPU's share
+    of the host's threads (created once, before the clock, each pinned to its
+    own physical core; the test5 pattern, one thread per byte-balanced message
+    slice; median of seven windows), and the reference's own
     benchmark loop (bmqp_crc32c.t.cpp:1116-1120: one message CRC'd up to
     100,000 times) for messages up to 1 MiB, beside its published figure."""
     import numpy as np
@@ -189,19 +204,32 @@ def cpu_baseline(lens_np, seed, seconds):
         offs[1:] = csum[:n - 1]
     nbytes = int(lens.sum(dtype=np.uint64))
     arena = oracle.fill_payload(0, nbytes, seed)
-    t1, reps1 = oracle.time_batch_for(arena, offs, lens, 1, "hw", 0.5)
-    # the multi-threaded leg shares the box's host with other jobs: three
-    # timed windows, the best one reported (interference only slows a
-    # window), all three listed
-    legs = [oracle.time_batch_for(arena, offs, lens, threads, "hw", max(0.5, seconds) / 3)
-            for _ in range(3)]
+    # every thread pinned to its own physical core of the process's allowed
+    # set, on the GPU's NUMA node first (round 6: unpinned, 16 threads swung
+    # 2x between windows of one run); the 1-thread leg on the
+    # first of them
+    node = gpu_numa_node(device)
+    cpus = oracle.pick_cpus(threads, node)
+    threads = len(cpus)
+    t1, reps1 = oracle.time_batch_for(arena, offs, lens, 1, "hw", 0.5, cpus=cpus)
+    # the multi-threaded leg shares the box's host with other jobs: seven
+    # timed windows, the median reported with the min and max
+    nwin = 7
+    legs = [oracle.time_batch_for(arena, offs, lens, threads, "hw", max(0.3, seconds / nwin),
+                                  cpus=cpus)
+            for _ in range(nwin)]
     gib = nbytes / 2**30
-    t, reps = min(legs, key=lambda tr: tr[0] / tr[1])
+    rates = sorted(gib * r / tt for tt, r in legs)
+    med = rates[nwin // 2]
     res = {
-        "value": round(gib * reps / t, 3),
+        "value": round(med, 3),
         "windows_GiBps": [round(gib * r / tt, 3) for tt, r in legs],
+        "window_min_max": [round(rates[0], 3), round(rates[-1], 3)],
+        "window_spread": round((rates[-1] - rates[0]) / med, 3),
         "unit": "GiB/s",
         "cores": threads,
+        "pinned_cpus": cpus,
+        "gpu_numa_node": node,
         "kind": "port",
         "single_thread_value": round(gib * reps1 / t1, 3),
         "host_threads": os.cpu_count(),
@@ -210,14 +238,14 @@ def cpu_baseline(lens_np, seed, seconds):
                         "(OMP_NUM_THREADS); the rest of the shared host is not ours to load"
                         % ((os.cpu_count() or 8) // 8, os.cpu_count() or 0, threads),
         "sample": "first %d msgs (%.0f MiB) of the same synthetic batch; %d threads (this "
-                  "GPU's share of the host: OMP_NUM_THREADS, 16 per GPU on the pool), created "
-                  "once before the clock, best of three windows: %d warm passes (%.2f s); "
-                  "single thread %d warm passes "
-                  "(%.2f s) = %.2f GiB/s; SSE4.2 crc32q 3-way interleaved, lanes joined by "
-                  "shift tables (bdlde::Crc32c default analogue, oracle/crc32c_oracle.c); "
+                  "GPU's share of the host: OMP_NUM_THREADS, 16 per GPU on the pool), each "
+                  "pinned to its own physical core (GPU NUMA node %s first), created once "
+                  "before the clock; median of %d windows of >= %.2f s; single thread %d warm "
+                  "passes (%.2f s) = %.2f GiB/s; SSE4.2 crc32q 3-way interleaved, lanes joined "
+                  "by shift tables (bdlde::Crc32c default analogue, oracle/crc32c_oracle.c); "
                   "host %s, nproc %d"
-                  % (n, gib * 1024, threads, reps, t, reps1, t1, gib * reps1 / t1, cpu_model(),
-                     os.cpu_count()),
+                  % (n, gib * 1024, threads, node, nwin, max(0.3, seconds / nwin), reps1, t1,
+                     gib * reps1 / t1, cpu_model(), os.cpu_count()),
     }
     size = int(lens_np[0]) if lens_np.size else 0
     if 0 < size <= (1 << 20) and bool(np.all(lens == size)):
@@ -519,8 +547,17 @@ def protocol(args):
 
 def pmc_traffic(config):
     """HBM bytes per k_fold launch from the newest committed rocprofv3 PMC
-    summary of this config (profiles/rNN/<config>_summary.json): read =
-    2 x FETCH_SIZE (gfx950 correction) + WRITE_SIZE, per MI355X_MICROARCH.md."""
+    summary of this config: read = 2 x FETCH_SIZE (gfx950 correction) +
+    WRITE_SIZE, per MI355X_MICROARCH.md.  bench_traffic.json (repo root,
+    written by tools/summarize_profiles.py) holds the newest figure per config
+    with its source summary under profiles/rNN/ -- it travels to the GPU box,
+    where ./profiles is not sent; the summaries themselves are the fallback."""
+    try:
+        with open(os.path.join(ROOT, "bench_traffic.json")) as f:
+            t = json.load(f)[config]
+        return int(t["traffic_bytes_per_launch"]), t["source"]
+    except (OSError, ValueError, KeyError, TypeError):
+        pass
     import glob
     # newest round first, and within a round its final/ set after the rest
     paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", config + "_summary.json")) +
@@ -829,7 +866,7 @@ def main():
                 strong["ranks_on_one_gpu"] = world
             res["strong_scaling"] = strong
         if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(lens_np, seed, args.cpu_seconds)
+            res["cpu_baseline"] = cpu_baseline(lens_np, seed, args.cpu_seconds, dev.index or 0)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

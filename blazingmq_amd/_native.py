@@ -78,6 +78,8 @@ lib.bmqcrc_fill_synthetic.argtypes = [_vp, _u64, _u64, _u64, ctypes.POINTER(Opts
 lib.bmqcrc_kernel_timing.restype = _int
 lib.bmqcrc_kernel_timing.argtypes = [_int, _vp, ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(_u32)]
+lib.bmqcrc_last_plan.restype = _int
+lib.bmqcrc_last_plan.argtypes = [_int, _vp, ctypes.POINTER(_u32)]
 lib.bmqcrc_last_launch.restype = _int
 lib.bmqcrc_last_launch.argtypes = [_int, _vp, ctypes.POINTER(_u32), ctypes.POINTER(_u32),
                                    ctypes.POINTER(_u32)]

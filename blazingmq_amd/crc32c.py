@@ -331,13 +331,16 @@ def kernel_timing(device, stream):
 
 def last_launch(device, stream):
     """Launch plan of the previous batch on (device, stream)
-    (bmqcrc_last_launch): dict(kernels, spec, seg_bytes) -- kernels launched
+    (bmqcrc_last_launch, bmqcrc_last_plan): dict(kernels, spec, seg_bytes,
+    map) -- kernels launched
     (1 = the fold alone), segments per message a single launch assumed (0 =
-    planned), segment size."""
+    planned), segment size, whether the planner built the size-class map."""
     k, u, sb = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
     _native.check(_native.lib.bmqcrc_last_launch(device, stream.cuda_stream, ctypes.byref(k),
                                                 ctypes.byref(u), ctypes.byref(sb)))
-    return {"kernels": k.value, "spec": u.value, "seg_bytes": sb.value}
+    m = ctypes.c_uint32()
+    _native.check(_native.lib.bmqcrc_last_plan(device, stream.cuda_stream, ctypes.byref(m)))
+    return {"kernels": k.value, "spec": u.value, "seg_bytes": sb.value, "map": m.value}
 
 
 def forget_shape(device, stream):

@@ -120,7 +120,7 @@ struct Workspace {
     uint32_t* hint_host = nullptr;
     uint32_t* hint_dev = nullptr;
     // Launch plan of the last batch (bmqcrc_last_launch).
-    uint32_t last_kernels = 0, last_spec = 0, last_seg = 0;
+    uint32_t last_kernels = 0, last_spec = 0, last_seg = 0, last_map = 0;
     // Given-up planner maps (hint_host[1], written by k_fold): the last epoch
     // seen, and how many more ragged batches take the meeting-free pair.
     uint32_t void_seen = 0, pair_left = 0;
@@ -461,7 +461,14 @@ int run_batch(Ctx& c, uint32_t flags, uint32_t seg, const void* arena, uint64_t 
             a.spec = hint_u;
         }
     }
-    if (!(kTuneBits & (16u | 4096u)) && !a.whole && !a.spec && a.map_planned && w->hint_host &&
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    const bool capturing = hipStreamIsCapturing(c.s, &cap) == hipSuccess &&
+                           cap == hipStreamCaptureStatusActive;
+    // A captured launch is replayed as recorded: the light planner's "the
+    // next batch gets the map" never happens inside a graph, so a capture
+    // keeps the map whatever the history
+    if (!(kTuneBits & (16u | 4096u)) && !capturing && !a.whole && !a.spec && a.map_planned &&
+        w->hint_host &&
         (__atomic_load_n(w->hint_host, __ATOMIC_RELAXED) & 0xffu) != kHintRagged &&
         !(host_max_len != UINT64_MAX && host_max_len > a.seg_bytes &&
           (host_min_len == 0 || (host_min_len - 1) / a.seg_bytes != (host_max_len - 1) / a.seg_bytes))) {
@@ -515,8 +522,7 @@ int run_batch(Ctx& c, uint32_t flags, uint32_t seg, const void* arena, uint64_t 
     if (!a.whole && !a.spec && a.map_planned) {
         // inside a graph capture every replay must tag its planner words
         // afresh: the tag then lives on the device (BatchArgs::plan_epoch 0)
-        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-        if (hipStreamIsCapturing(c.s, &cap) == hipSuccess && cap == hipStreamCaptureStatusActive) {
+        if (capturing) {
             a.plan_epoch = 0;
         }
     }
@@ -551,6 +557,7 @@ int run_batch(Ctx& c, uint32_t flags, uint32_t seg, const void* arena, uint64_t 
                       : !a.map_planned       ? 2u
                       : single_pass_planner(a) ? 2u
                                              : 3u;
+    w->last_map = n != 0 && !a.whole && !a.spec && a.map_planned ? 1u : 0u;
     return 0;
 }
 
@@ -617,15 +624,10 @@ int parse_opts(const bmqcrc_opts* opts, bmqcrc_opts* o, uint32_t* seg, int* dev)
     if (opts) {
         // struct_size 0 reads only the ABI 2.0 fields: a caller that never set
         // it may be built against any earlier, shorter layout
+        // (ABI 2.7: nothing past offsetof(ndevices) is read then, not even to
+        // check it -- a 2.0 caller's struct ends there)
         const size_t given = opts->struct_size ? opts->struct_size : offsetof(bmqcrc_opts, ndevices);
         memcpy(o, opts, std::min<size_t>(sizeof(*o), given));
-        // ABI 2.1-2.4 read the whole struct when struct_size was 0: a caller
-        // of those minors that zero-initialised it, set a later field and
-        // never set struct_size would now lose that field silently -- refuse
-        if (!opts->struct_size && (opts->ndevices || opts->max_len || opts->min_len)) {
-            return fail(BMQCRC_EINVAL, "bmqcrc_opts.struct_size is 0 but a field past ABI 2.0 "
-                                       "(ndevices, max_len, min_len) is set: set struct_size");
-        }
         o->struct_size = sizeof(*o);
     }
     *seg = o->seg_bytes;
@@ -1642,6 +1644,22 @@ int bmqcrc_last_launch(int device, void* stream, uint32_t* kernels, uint32_t* sp
     return 0;
 }
 
+int bmqcrc_last_plan(int device, void* stream, uint32_t* map)
+{
+    t_err.clear();
+    DeviceGuard keep_device;
+    int dev, rc;
+    if ((rc = resolve_device(device, &dev))) {
+        return rc;
+    }
+    Workspace* w = workspace(dev, stream);
+    std::lock_guard<std::mutex> g(w->mu);
+    if (map) {
+        *map = w->last_map;
+    }
+    return 0;
+}
+
 int bmqcrc_forget_shape(int device, void* stream)
 {
     t_err.clear();
@@ -1759,7 +1777,7 @@ uint64_t bmqcrc_host_fallbacks(int32_t* last_rc)
 
 uint32_t bmqcrc_version(void)
 {
-    return (2u << 16) | 6u;
+    return (2u << 16) | 7u;
 }
 
 }  // extern "C"

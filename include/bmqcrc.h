@@ -63,9 +63,10 @@ extern "C" {
 
 typedef struct bmqcrc_opts {
     uint32_t struct_size; /* sizeof(bmqcrc_opts); 0 reads the ABI 2.0 fields only (device,
-                             stream, flags, seg_bytes): set it to use anything later
-                             (ABI 2.6: 0 with ndevices, max_len or min_len set is
-                             BMQCRC_EINVAL, where 2.1-2.4 read the whole struct) */
+                             stream, flags, seg_bytes) and never touches the bytes
+                             after them, so a 2.0 caller's 24-byte struct is safe:
+                             set it to use anything later (ABI 2.1-2.4 read the
+                             whole struct when it was 0; such callers must set it) */
     int32_t device;       /* HIP device ordinal; -1 = current device */
     void* stream;         /* hipStream_t; NULL = that device's default (null) stream */
     uint32_t flags;       /* BMQCRC_F_* */
@@ -197,6 +198,13 @@ int bmqcrc_kernel_timing(int device, void* stream, double* total_ms, uint32_t* c
  * the segment size used.  Any pointer may be NULL. */
 int bmqcrc_last_launch(int device, void* stream, uint32_t* kernels, uint32_t* spec,
                        uint32_t* seg_bytes);
+
+/* ABI 2.7.  Whether the previous planned batch on (device, stream) had its
+ * size-class map built (*map = 1: k_plan_map, or k_plan + k_plan_sort) or
+ * was planned by the light k_plan alone, whose fold searches the
+ * per-message segment offsets (*map = 0; also for single-launch batches).
+ * A batch captured into a graph always gets the map. */
+int bmqcrc_last_plan(int device, void* stream, uint32_t* map);
 
 /* ABI 2.2.  Drop the batch-shape prediction of (device, stream): the next
  * batch there is planned (k_plan runs) instead of being launched on the guess

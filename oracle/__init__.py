@@ -41,6 +41,9 @@ def lib():
         L.oracle_time_batch.restype = ctypes.c_double
         L.oracle_time_batch.argtypes = [vp, vp, vp, vp, vp, ctypes.c_size_t, ctypes.c_int,
                                         ctypes.c_int, ctypes.c_int]
+        L.oracle_time_batch_pinned.restype = ctypes.c_double
+        L.oracle_time_batch_pinned.argtypes = [vp, vp, vp, vp, vp, ctypes.c_size_t, ctypes.c_int,
+                                               ctypes.c_int, ctypes.c_int, vp]
         L.oracle_time_repeat.restype = ctypes.c_double
         L.oracle_time_repeat.argtypes = [vp, u32, ctypes.c_int, ctypes.c_int,
                                          ctypes.POINTER(u32)]
@@ -90,25 +93,65 @@ def batch(arena, offsets, lengths, seeds=None, nthreads=1, variant="hw"):
     return out
 
 
-def time_batch(arena, offsets, lengths, nthreads, variant="hw", reps=1):
+def time_batch(arena, offsets, lengths, nthreads, variant="hw", reps=1, cpus=None):
+    """cpus: optional list of nthreads CPU ids, thread t pinned to cpus[t]."""
     a = np.ascontiguousarray(arena).view(np.uint8)
     off = np.ascontiguousarray(offsets, dtype=np.uint64)
     ln = np.ascontiguousarray(lengths, dtype=np.uint32)
     out = np.empty(off.size, dtype=np.uint32)
-    t = lib().oracle_time_batch(a.ctypes.data, off.ctypes.data, ln.ctypes.data, None,
-                                out.ctypes.data, off.size, nthreads, VARIANTS[variant], reps)
+    pin = None
+    if cpus is not None:
+        assert len(cpus) >= nthreads
+        pin = np.ascontiguousarray(cpus[:nthreads], dtype=np.int32)
+    t = lib().oracle_time_batch_pinned(a.ctypes.data, off.ctypes.data, ln.ctypes.data, None,
+                                       out.ctypes.data, off.size, nthreads, VARIANTS[variant],
+                                       reps, None if pin is None else pin.ctypes.data)
     return t, out
 
 
-def time_batch_for(arena, offsets, lengths, nthreads, variant="hw", seconds=0.5):
+def time_batch_for(arena, offsets, lengths, nthreads, variant="hw", seconds=0.5, cpus=None):
     """Passes over the batch on `nthreads` threads (created once, one untimed
     warm-up pass) until about `seconds` of timed work: (seconds, passes)."""
-    t, _ = time_batch(arena, offsets, lengths, nthreads, variant, 1)
+    t, _ = time_batch(arena, offsets, lengths, nthreads, variant, 1, cpus)
     reps = 1
     while t < seconds:  # at most a few rounds: each aims 20 % past the target
         reps = max(reps + 1, int(1.2 * seconds * reps / max(t, 1e-7)))
-        t, _ = time_batch(arena, offsets, lengths, nthreads, variant, reps)
+        t, _ = time_batch(arena, offsets, lengths, nthreads, variant, reps, cpus)
     return t, reps
+
+
+def pick_cpus(nthreads, numa_node=None):
+    """Up to nthreads CPUs from this process's allowed set, one per physical
+    core (SMT siblings skipped), preferring `numa_node`'s cores (the GPU's
+    node).  Returns the list (shorter if the set holds fewer cores)."""
+    allowed = sorted(os.sched_getaffinity(0))
+
+    def read(path, default):
+        try:
+            with open(path) as f:
+                return f.read().strip()
+        except OSError:
+            return default
+
+    def node_of(c):
+        base = "/sys/devices/system/cpu/cpu%d" % c
+        try:
+            for e in os.listdir(base):
+                if e.startswith("node") and e[4:].isdigit():
+                    return int(e[4:])
+        except OSError:
+            pass
+        return -1
+
+    seen, first, rest = set(), [], []
+    for c in allowed:
+        topo = "/sys/devices/system/cpu/cpu%d/topology/" % c
+        core = (read(topo + "physical_package_id", "0"), read(topo + "core_id", str(c)))
+        if core in seen:
+            continue
+        seen.add(core)
+        (first if numa_node is None or node_of(c) == numa_node else rest).append(c)
+    return (first + rest)[:nthreads]
 
 
 def time_repeat(buf, iters, variant="hw"):

@@ -33,10 +33,12 @@
  * Parity of all variants is pinned by tests/golden/ (the reference's golden
  * vectors) in tests/test_oracle_golden.py.
  */
+#define _GNU_SOURCE 1 /* pthread_setaffinity_np: the pinned CPU-baseline pool */
 #include <stddef.h>
 #include <stdint.h>
 #include <string.h>
 #include <pthread.h>
+#include <sched.h>
 #include <time.h>
 
 #if defined(__x86_64__)
@@ -383,11 +385,23 @@ struct pool_arg {
     struct batch_job *job;
     pthread_barrier_t *bar;
     int passes;
+    int cpu; /* < 0: not pinned */
 };
+
+static void pin_self(int cpu)
+{
+    if (cpu >= 0 && cpu < CPU_SETSIZE) {
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        CPU_SET(cpu, &set);
+        pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+    }
+}
 
 static void *pool_worker(void *arg)
 {
     struct pool_arg *p = (struct pool_arg *)arg;
+    pin_self(p->cpu);
     for (int r = 0; r < p->passes; ++r) {
         pthread_barrier_wait(p->bar);
         batch_worker(p->job);
@@ -405,10 +419,11 @@ static double now_s(void)
 
 /* Wall-clock seconds for `reps` passes over the batch on `nthreads` threads
  * (bench helper): threads created before the clock starts and one untimed
- * warm-up pass first. */
-double oracle_time_batch(const uint8_t *arena, const uint64_t *off, const uint32_t *len,
-                         const uint32_t *seed, uint32_t *out, size_t n, int nthreads,
-                         int variant, int reps)
+ * warm-up pass first.  cpus (may be NULL): thread t runs pinned to cpus[t]
+ * (thread 0 is the caller, whose affinity is restored afterwards). */
+double oracle_time_batch_pinned(const uint8_t *arena, const uint64_t *off, const uint32_t *len,
+                                const uint32_t *seed, uint32_t *out, size_t n, int nthreads,
+                                int variant, int reps, const int *cpus)
 {
     nthreads = clamp_threads(nthreads);
     pthread_once(&g_tab_once, init_tables);
@@ -423,7 +438,13 @@ double oracle_time_batch(const uint8_t *arena, const uint64_t *off, const uint32
         args[t].job = &jobs[t];
         args[t].bar = &bar;
         args[t].passes = passes;
+        args[t].cpu = cpus ? cpus[t] : -1;
         pthread_create(&th[t], NULL, pool_worker, &args[t]);
+    }
+    cpu_set_t saved;
+    const int restore = cpus && pthread_getaffinity_np(pthread_self(), sizeof(saved), &saved) == 0;
+    if (cpus) {
+        pin_self(cpus[0]);
     }
     double t0 = 0;
     for (int r = 0; r < passes; ++r) {
@@ -439,7 +460,17 @@ double oracle_time_batch(const uint8_t *arena, const uint64_t *off, const uint32
         pthread_join(th[t], NULL);
     }
     pthread_barrier_destroy(&bar);
+    if (restore) {
+        pthread_setaffinity_np(pthread_self(), sizeof(saved), &saved);
+    }
     return dt;
+}
+
+double oracle_time_batch(const uint8_t *arena, const uint64_t *off, const uint32_t *len,
+                         const uint32_t *seed, uint32_t *out, size_t n, int nthreads,
+                         int variant, int reps)
+{
+    return oracle_time_batch_pinned(arena, off, len, seed, out, n, nthreads, variant, reps, NULL);
 }
 
 /* The reference's own benchmark loop (bmqp_crc32c.t.cpp:1116-1120): one

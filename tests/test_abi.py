@@ -56,28 +56,33 @@ def test_library_contains_gfx950_code_object(tmp_path):
 def test_version_and_error_string():
     lib = ctypes.CDLL(LIB)
     lib.bmqcrc_version.restype = ctypes.c_uint32
-    assert lib.bmqcrc_version() >> 16 == 2 and lib.bmqcrc_version() & 0xffff >= 5
+    assert lib.bmqcrc_version() >> 16 == 2 and lib.bmqcrc_version() & 0xffff >= 7
     lib.bmqcrc_last_error.restype = ctypes.c_char_p
     assert isinstance(lib.bmqcrc_last_error(), bytes)
 
 
-def test_zero_struct_size_with_later_fields_is_refused():
-    # struct_size 0 reads the ABI 2.0 fields only; a caller that also set a
-    # later field (as ABI 2.1-2.4 read them) gets EINVAL, not a silent drop.
-    # The check precedes any device lookup, so it runs without a GPU.
+def test_zero_struct_size_reads_only_the_abi20_fields():
+    # struct_size 0 is an ABI 2.0 caller, whose struct ends at ndevices (24
+    # bytes): the library must not read past it.  Put the 2.0 fields at the
+    # front of a larger buffer whose later bytes are garbage that would be an
+    # invalid ndevices / max_len / min_len, and check the call is not
+    # refused for them: ENODEV without a GPU, a computed CRC with one.
     from blazingmq_amd import _native as N
-    buf = (ctypes.c_uint8 * 64)()
+    assert N.Opts.ndevices.offset == 24
+    payload = (ctypes.c_uint8 * 64)(*range(64))
     offs = (ctypes.c_uint64 * 1)(0)
     lens = (ctypes.c_uint32 * 1)(8)
     out = (ctypes.c_uint32 * 1)()
-    for field in ("ndevices", "max_len", "min_len"):
-        o = N.make_opts(**{field: 2} if field != "ndevices" else {})
-        if field == "ndevices":
-            o.ndevices = 2
-        o.struct_size = 0
-        rc = N.lib.bmqcrc_crc32c_batch(buf, 64, offs, lens, None, out, 1, ctypes.byref(o))
-        assert rc == N.BMQCRC_EINVAL, (field, rc)
-        assert b"struct_size" in N.lib.bmqcrc_last_error()
+    raw = (ctypes.c_uint8 * ctypes.sizeof(N.Opts))()
+    ctypes.memset(raw, 0xA5, ctypes.sizeof(raw))
+    v20 = N.make_opts()
+    v20.struct_size = 0
+    ctypes.memmove(raw, ctypes.byref(v20), 24)
+    rc = N.lib.bmqcrc_crc32c_batch(payload, 64, offs, lens, None, out, 1,
+                                   ctypes.cast(raw, ctypes.POINTER(N.Opts)))
+    assert rc in (0, N.BMQCRC_ENODEV), (rc, N.lib.bmqcrc_last_error())
+    if rc == 0:
+        assert out[0] == N.lib.bmqcrc_crc32c(payload, 8, 0)
 
 
 def test_opts_layout_matches_the_header(tmp_path):

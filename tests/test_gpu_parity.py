@@ -419,7 +419,8 @@ def test_shape_hint_misprediction(cuda):
         run(lens)
 
 
-def test_planner_map_given_up(cuda, record_property):
+@pytest.mark.perf
+def test_planner_map_given_up(cuda, record_property, perf_bound):
     # Ragged batches are planned by one kernel whose blocks meet once,
     # grid-wide.  When they cannot all run at once a block stops waiting after
     # bmqcrc_plan_wait's limit and the map is given up; every block still
@@ -480,9 +481,10 @@ def test_planner_map_given_up(cuda, record_property):
     print("mapped %.3f ms, given up %.3f ms per batch" % (1e3 * t_map, 1e3 * t_void))
     record_property("given_up_over_mapped", round(t_void / t_map, 3))
     # DESIGN.md 4 claims 1.14x on Zipf; the wall clock here includes the
-    # launch and synchronisation overhead common to both, so the margin is
-    # 1.3x plus 0.2 ms
-    assert t_void < 1.3 * t_map + 2e-4, (t_map, t_void)
+    # launch and synchronisation overhead common to both, so the bound is
+    # 1.3x plus 0.2 ms (asserted under -m perf only, recorded always)
+    perf_bound("given_up_within_1.3x", t_void < 1.3 * t_map + 2e-4,
+               {"t_map_ms": round(1e3 * t_map, 3), "t_void_ms": round(1e3 * t_void, 3)})
     run()  # back to mapping
     assert plan_wait(cuda.index, s) == v1
 

@@ -106,6 +106,41 @@ def test_graph_replays_of_a_ragged_batch_with_new_lengths(cuda):
         assert bad.size == 0, (it, bad[:8])
 
 
+def test_graph_capture_on_a_fresh_stream_keeps_the_map(cuda):
+    # With no shape history a planned batch gets the light k_plan, whose fold
+    # searches seg_first, and the stream's NEXT batch gets the map -- which
+    # never happens inside a graph.  A capture therefore plans with the map
+    # whatever the history, and the replays stay exact.
+    import torch
+    from blazingmq_amd import last_launch
+    rng = np.random.default_rng(36)
+    size, n = 16 << 20, 60_000
+    side = torch.cuda.Stream(cuda)
+    lens = np.concatenate([rng.integers(0, 300, size=n - 100),
+                           rng.integers(0, 40000, size=100)]).astype(np.uint32)
+    rng.shuffle(lens)
+    offs = (rng.random(n) * (size - lens + 1)).astype(np.int64)
+    data = rng.integers(0, 256, size=size, dtype=np.uint8)
+    arena = torch.from_numpy(data).to(cuda)
+    o = torch.from_numpy(offs).to(cuda)
+    ln = torch.from_numpy(lens.view(np.int32)).to(cuda)
+    out = torch.zeros(n, dtype=torch.int32, device=cuda)
+    reserve(cuda.index or 0, side, n, size, 2048)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        Crc32c.calculate_batch(arena, o, ln, None, out, stream=side, sync=False, seg_bytes=2048)
+    launch = last_launch(cuda.index or 0, side)
+    assert launch["spec"] == 0 and launch["map"] == 1, launch
+    exp = oracle.batch(data, offs, lens, None, nthreads=8)
+    for it in range(3):
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        bad = np.nonzero(out.cpu().numpy().view(np.uint32) != exp)[0]
+        assert bad.size == 0, (it, bad[:8])
+
+
 def test_graph_capture_while_the_pair_plans(cuda):
     # A given-up map switches the workspace to the pair planner (k_plan +
     # k_plan_sort) for its next ragged batches.  A batch captured then carries
@@ -287,7 +322,9 @@ def test_concurrent_gather_and_multi_device_walks(cuda):
     assert not errors, errors
 
 
-def test_processes_share_the_planner_on_one_gpu(cuda, record_property, tmp_path):
+@pytest.mark.perf
+def test_processes_share_the_planner_on_one_gpu(cuda, record_property, perf_bound,
+                                                tmp_path):
     """Three processes CRC ragged batches of 1.4M+ messages on the same GPU at
     once, with the default planner wait limit (tests/mp_planner_worker.py).
     The single-pass planner's blocks meet grid-wide, so with other processes'
@@ -336,4 +373,5 @@ def test_processes_share_the_planner_on_one_gpu(cuda, record_property, tmp_path)
     print("alone %.3f ms, three processes %s ms, given-up maps %s"
           % (alone["median_ms"], [round(r["median_ms"], 3) for r in shared],
              [r["plan_voided"] for r in shared]))
-    assert worst <= 1.3 * share + 0.5, (alone, shared)
+    perf_bound("shared_within_1.3x_of_share", worst <= 1.3 * share + 0.5,
+               {"alone_ms": alone["median_ms"], "worst_shared_ms": worst})

@@ -10,6 +10,9 @@
                               half the bytes of a wide coalesced stream,
                               MI355X_MICROARCH.md HBM), algorithmic bytes.
 
+Also records each config's traffic in bench_traffic.json (repo root), the
+file bench.py's roofline.traffic reads on the GPU box.
+
 usage: summarize_profiles.py <round dir> <prefix> <config>=<alg_bytes> ...
 """
 import csv
@@ -19,6 +22,27 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+TRAFFIC = os.path.join(ROOT, "bench_traffic.json")
+
+
+def record_traffic(cfg, s, summary_path):
+    """bench_traffic.json (tracked, at the repo root so that it travels to
+    the GPU box, where ./profiles is not sent): the newest PMC traffic per
+    config, which bench.py's roofline.traffic reports with its source."""
+    try:
+        with open(TRAFFIC) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        t = {}
+    t[cfg] = {"traffic_bytes_per_launch": int(s["traffic_bytes_per_launch"]),
+              "alg_bytes_per_launch": int(s["alg_bytes_per_launch"]),
+              "traffic_over_alg": round(s["traffic_over_alg"], 5),
+              "source": os.path.relpath(summary_path, ROOT)}
+    with open(TRAFFIC, "w") as f:
+        json.dump(t, f, indent=1, sort_keys=True)
+        f.write("\n")
 
 
 def main(argv):
@@ -55,6 +79,7 @@ def main(argv):
              "achieved_alg_GBps": alg / avg_us / 1e3}
         with open(os.path.join(out_dir, cfg + "_summary.json"), "w") as f:
             json.dump(s, f, indent=1)
+        record_traffic(cfg, s, os.path.join(out_dir, cfg + "_summary.json"))
         print(cfg, "avg %.1f us" % avg_us, "traffic/alg %.4f" % s["traffic_over_alg"],
               "alg %.0f GB/s" % s["achieved_alg_GBps"])
 
