@@ -90,6 +90,11 @@ def parse():
     p.add_argument("--msgs", type=int, default=0,
                    help="experiment: override the message count of a uniform config "
                         "(the line is then marked as not the BASELINE workload)")
+    p.add_argument("--align", type=int, default=0,
+                   help="experiment: start every message at a multiple of this many bytes "
+                        "(padding between messages, never read; Zipf over-fetch attribution: "
+                        "128 leaves no 128-byte line shared by two messages); the line is "
+                        "marked as not the BASELINE workload")
     p.add_argument("--shard", default="",
                    help="experiment 'i/N': time only shard i of an N-way split of the config on "
                         "this one GPU (a strong-scaling rank's work; the line is marked as not "
@@ -660,16 +665,22 @@ def main():
         lens_np, begin = gen(rank, world)
     n = int(lens_np.size)
     offs_np = np.zeros(n, dtype=np.int64)
+    span = lens_np.astype(np.int64)
+    if args.align > 1:
+        span = (span + args.align - 1) // args.align * args.align
+        desc = "EXPERIMENT (not the BASELINE workload): %s, messages %d-byte aligned" % (
+            desc, args.align)
     if n > 1:
-        np.cumsum(lens_np[:-1], dtype=np.int64, out=offs_np[1:])
+        np.cumsum(span[:-1], dtype=np.int64, out=offs_np[1:])
     total_bytes = int(lens_np.sum(dtype=np.uint64))
+    arena_bytes = int(offs_np[-1] + lens_np[-1]) if n else 0
     # This rank's messages are bytes [begin, begin + total) of synthetic stream
     # `seed`, generated in HBM; offsets are relative to the rank's arena.
     stream = torch.cuda.current_stream(dev)
     rotate = max(1, args.rotate)
     copies = []  # --rotate: N independent copies of the batch, one per step in turn
     for _ in range(rotate):
-        arena = torch.empty(max(total_bytes, 8), dtype=torch.uint8, device=dev)
+        arena = torch.empty(max(arena_bytes, 8), dtype=torch.uint8, device=dev)
         _fill_slice(bmq, arena, seed, begin)
         copies.append((arena, torch.from_numpy(offs_np).to(dev),
                        torch.from_numpy(lens_np.view(np.int32)).to(dev),

@@ -662,6 +662,40 @@ __device__ __forceinline__ void dma_round(uint32_t lds_dst, const uint64_t (&pba
         : "memory", "scc");
 }
 
+// LDS-DMA of whole KiB from global memory (the remainder and un-shift tables
+// of the one-segment kernel's prologue): instruction i copies 1 KiB, every
+// lane 16 B, to lds_dst + 1024 i.  Lanes outside exec copy nothing.
+template <int N>
+__device__ __forceinline__ void dma_copy_kib(uint32_t lds_dst, uint64_t src)
+{
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const uint64_t s = src + 1024u * (uint32_t)i + 16u * (uint32_t)__lane_id();
+        uint32_t keep;
+        asm volatile("s_waitcnt lgkmcnt(0)\n\t"
+                     "s_mov_b32 %0, m0\n\t"
+                     "s_mov_b32 m0, %1\n\t"
+                     "s_nop 0\n\t"
+                     "global_load_lds_dwordx4 %2, off\n\t"
+                     "s_mov_b32 m0, %0\n\t"
+                     : "=&s"(keep)
+                     : "s"(lds_dst + 1024u * (uint32_t)i), "v"(s)
+                     : "memory", "scc");
+    }
+}
+
+#ifndef BMQCRC_ONE_EARLY
+#define BMQCRC_ONE_EARLY 1  // the one-segment kernel issues its first group's loads before its
+                            // tables (LDS-DMA'd behind them, one barrier before the first
+                            // lookup); 0: tables first, through VGPRs, and a barrier (A/B)
+#endif
+constexpr bool kOneEarly = BMQCRC_ONE_EARLY == 1;
+#ifndef BMQCRC_DESC_FIRST
+#define BMQCRC_DESC_FIRST 1  // the first group's descriptors before the prologue's table loads
+                             // (every k_fold); 0: after them (round 5; A/B)
+#endif
+constexpr bool kDescFirst = BMQCRC_DESC_FIRST != 0;
+
 #ifndef BMQCRC_GROUP_DESC
 #define BMQCRC_GROUP_DESC 1  // 0: every seginfo entry written (round 3; A/B)
 #endif
@@ -1150,9 +1184,27 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     // and for identity batches; discarded otherwise).
     constexpr int kTw = (kTab / 4) / (int)kThreads, kXw = 1024 / kThreads;  // table words per thread
     static_assert(kTw * (int)kThreads * 4 == kTab && kXw * kThreads == 1024, "table fill");
-    uint32_t tw[kTw];
+    // The one-segment kernel (kOneEarly) loads no table here: its first
+    // group's descriptors go out first, then the group's data, and only then
+    // the tables, LDS-DMA'd (see early_tables below), so the first data
+    // load no longer waits behind 8-24 KiB of table loads and a barrier
+    // (per-wave stamps, 20,000 x 256 B: prologue 0.8-1.0 us, first issue
+    // 1.5 us later, profiles/r05/probe/fold_trace_small_batches.jsonl)
+    constexpr bool kEarly = ONE && kOneEarly;
+    static_assert(!kEarly || kTab % (1024 * WPB) == 0, "early tables: whole KiB per wave");
+    // the wave's first group (claim k = wave, see gid below), as if
+    // segment = message: its descriptors are the kernel's first loads
+    // (round 6; before, 8-24 KiB of table loads per block went out first
+    // and every wave's first data load queued behind them)
+    const uint32_t gfirst = a.spread ? wave * gridDim.x + blockIdx.x : blockIdx.x * WPB + wave;
+    const uint32_t sid = gfirst * 64u + (uint32_t)lane;
+    [[maybe_unused]] SegDesc spec = {0ull, 0u, 0u, 0u, 0u};
+    if constexpr (kDescFirst) {
+        spec = fetch_desc(a, SegRef{sid, 0u}, sid < a.n);
+    }
+    uint32_t tw[kEarly ? 1 : kTw];
 #pragma unroll
-    for (int i = 0; i < kTw; ++i) {
+    for (int i = 0; i < (kEarly ? 0 : kTw); ++i) {
         const uint32_t t = threadIdx.x + (uint32_t)i * kThreads;
         if constexpr (H11) {
             tw[i] = c_rtab11[t];
@@ -1185,25 +1237,48 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     }
     // x^(-8p) un-shift table -> LDS too: a per-lane index, so from constant
     // memory it would be a vector load with a full memory latency per group
-    __shared__ uint32_t xneg8[136];
-    const uint32_t xn = threadIdx.x < 136u ? c_xneg8[threadIdx.x] : 0u;
+    __shared__ __attribute__((aligned(16))) uint32_t xneg8[136];
+    const uint32_t xn = (!kEarly && threadIdx.x < 136u) ? c_xneg8[threadIdx.x] : 0u;
     [[maybe_unused]] const uint32_t g0 = blockIdx.x * WPB + wave;  // this wave's index in the grid
     FOLD_STAMP(0)
-    // the wave's first group (claim k = wave, see gid below), as if
-    // segment = message
-    const uint32_t gfirst = a.spread ? wave * gridDim.x + blockIdx.x : blockIdx.x * WPB + wave;
-    const uint32_t sid = gfirst * 64u + (uint32_t)lane;
-    const SegDesc spec = fetch_desc(a, SegRef{sid, 0u}, sid < a.n);
+    if constexpr (!kDescFirst) {
+        spec = fetch_desc(a, SegRef{sid, 0u}, sid < a.n);
+    }
     // remainder-reduction tables -> LDS (8 KiB, once per block; no DMA in
     // flight yet; plan_reduce's barriers order them before any lookup)
 #pragma unroll
-    for (int i = 0; i < kTw; ++i) {
+    for (int i = 0; i < (kEarly ? 0 : kTw); ++i) {
         const uint32_t t = threadIdx.x + (uint32_t)i * kThreads;
         *(lds_u32*)(uintptr_t)(tab_lds + 4u * t) = tw[i];
     }
-    if (threadIdx.x < 136u) {
+    if (!kEarly && threadIdx.x < 136u) {
         xneg8[threadIdx.x] = xn;
     }
+    // kEarly: this wave's share of the tables, LDS-DMA'd after its first
+    // group's loads (wave w: KiB w * kTab / 1024 / WPB ...; wave 0 also the
+    // 544-byte x^-8p table).  Nothing reads them before early_barrier.
+    auto early_tables = [&]() {
+        if constexpr (kEarly) {
+            constexpr int kKib = kTab / 1024 / WPB;
+            const uint64_t src = H11 ? (uint64_t)(uintptr_t)&c_rtab11[0]
+                                     : (uint64_t)(uintptr_t)&c_ty[0][0];
+            dma_copy_kib<kKib>(tab_lds + 1024u * kKib * wave, src + 1024u * kKib * wave);
+            if (wave == 0 && lane < 34) {
+                dma_copy_kib<1>((uint32_t)(uintptr_t)xneg8, (uint64_t)(uintptr_t)&c_xneg8[0]);
+            }
+        }
+    };
+    // every wave once: its own table loads have landed (a counted wait of
+    // its fold, or the explicit one here), then the block meets, so every
+    // wave's share is visible before any lookup
+    auto early_barrier = [&](bool wait) {
+        if constexpr (kEarly) {
+            if (wait) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __builtin_amdgcn_s_barrier();
+        }
+    };
     if (!ONE) {
 #pragma unroll
         for (int i = 0; i < kXw; ++i) {
@@ -1221,7 +1296,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
                      0u};
     if (!whole && !spec_mode) {
         pt = plan_reduce(a, &pl, pw);
-    } else {
+    } else if (!kEarly) {
         __syncthreads();
     }
     // more segments than 32-bit indices hold: every message in one lane.  A
@@ -1740,15 +1815,34 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
             if (sorted) {
                 r1 = resolve_sorted(r1, v1);
             }
-            nxt = fetch_desc(a, r1, v1);
+            if constexpr (!kEarly) {
+                nxt = fetch_desc(a, r1, v1);
+            }
             const uint32_t s2 = (g + 2u * stride) * 64u + (uint32_t)lane;
             ref2 = map_segment(a, &pl, s2, g + 2u * stride < ngroups && s2 < total, identity, uni,
                                sorted, ep);
             setup(d0, g, G);
+            if constexpr (kEarly) {
+                // a wait the compiler sees (vmcnt(0), expcnt/lgkmcnt free):
+                // none of its loads is pending past here, so its own waits
+                // inside the loop stay where they were (without it, one
+                // landed right after the fold's counted vmcnt(8) and
+                // serialized every group's rounds); nothing but this group's
+                // descriptors is in flight yet, so it costs nothing
+                __builtin_amdgcn_s_waitcnt(0x0F70);
+            }
             issue_first_rounds(G);
+            early_tables();
+            if constexpr (kEarly) {
+                nxt = fetch_desc(a, r1, v1);  // behind the first data, not in front of it
+            }
             FOLD_STAMP(2)
+        } else {
+            early_tables();
+            early_barrier(true);
         }
         [[maybe_unused]] bool first = true;
+        bool meet = kEarly;  // early_barrier still owed (after the first group's fold)
         [[maybe_unused]] uint32_t it = 0;
         Pending pend = {0u, 0u, 0u};
         for (; g < ngroups; g += stride) {
@@ -1780,6 +1874,10 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
             }
             uint32_t Rm[32];
             fold_rounds(G, Rm);
+            if (meet) {  // (fold_rounds ended on vmcnt(0): this wave's tables are in)
+                early_barrier(false);
+                meet = false;
+            }
 #if BMQCRC_FOLD_DIAG
             if (first) {
                 FOLD_STAMP(3)

@@ -302,7 +302,7 @@ def test_config_1k_x_4KiB_planned_then_speculative(cuda):
     planned = run()
     assert planned["spec"] == 0 and planned["kernels"] >= 2 and planned["seg_bytes"] == 256
     for _ in range(3):
-        assert run() == {"kernels": 1, "spec": 16, "seg_bytes": 256}
+        assert run() == {"kernels": 1, "spec": 16, "seg_bytes": 256, "map": 0}
     forget_shape(cuda.index, s)
     assert run()["spec"] == 0                   # planned again, then speculative again
     assert run()["spec"] == 16
@@ -318,7 +318,7 @@ def test_config_1k_x_4KiB_planned_then_speculative(cuda):
 
     for _ in range(3):
         forget_shape(cuda.index, s)
-        assert declared() == {"kernels": 1, "spec": 16, "seg_bytes": 256}
+        assert declared() == {"kernels": 1, "spec": 16, "seg_bytes": 256, "map": 0}
 
 
 def test_config_1M_x_256B_full(cuda):
