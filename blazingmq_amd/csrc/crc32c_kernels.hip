@@ -1190,7 +1190,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     // load no longer waits behind 8-24 KiB of table loads and a barrier
     // (per-wave stamps, 20,000 x 256 B: prologue 0.8-1.0 us, first issue
     // 1.5 us later, profiles/r05/probe/fold_trace_small_batches.jsonl)
-    constexpr bool kEarly = ONE && kOneEarly;
+    constexpr bool kEarly = ONE && kOneEarly && WPB == 4;
     static_assert(!kEarly || kTab % (1024 * WPB) == 0, "early tables: whole KiB per wave");
     // the wave's first group (claim k = wave, see gid below), as if
     // segment = message: its descriptors are the kernel's first loads
@@ -1268,9 +1268,9 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
             }
         }
     };
-    // every wave once: its own table loads have landed (a counted wait of
-    // its fold, or the explicit one here), then the block meets, so every
-    // wave's share is visible before any lookup
+    // every wave once, before its first lookup: its own table loads have
+    // landed (the counted waits of its first fold, or the explicit one
+    // here), then the block meets, so every wave's share is visible
     auto early_barrier = [&](bool wait) {
         if constexpr (kEarly) {
             if (wait) {
@@ -1296,7 +1296,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
                      0u};
     if (!whole && !spec_mode) {
         pt = plan_reduce(a, &pl, pw);
-    } else if (!kEarly) {
+    } else {
         __syncthreads();
     }
     // more segments than 32-bit indices hold: every message in one lane.  A
@@ -1842,7 +1842,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
             early_barrier(true);
         }
         [[maybe_unused]] bool first = true;
-        bool meet = kEarly;  // early_barrier still owed (after the first group's fold)
+        bool meet = kEarly;  // early_barrier owed, after the first group's fold
         [[maybe_unused]] uint32_t it = 0;
         Pending pend = {0u, 0u, 0u};
         for (; g < ngroups; g += stride) {
