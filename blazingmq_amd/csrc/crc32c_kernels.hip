@@ -690,6 +690,13 @@ __device__ __forceinline__ void dma_copy_kib(uint32_t lds_dst, uint64_t src)
                             // lookup); 0: tables first, through VGPRs, and a barrier (A/B)
 #endif
 constexpr bool kOneEarly = BMQCRC_ONE_EARLY == 1;
+#ifndef BMQCRC_ROUND_WAIT
+#define BMQCRC_ROUND_WAIT 0  // a round's fold first waits for every load issued before it
+                             // (the next round landed too, the one after issued once the
+                             // line is read); 8: for its own 8 loads only, the next round
+                             // still landing while it folds (round 5; A/B)
+#endif
+constexpr bool kRoundWait0 = BMQCRC_ROUND_WAIT == 0;
 #ifndef BMQCRC_DESC_FIRST
 #define BMQCRC_DESC_FIRST 1  // the first group's descriptors before the prologue's table loads
                              // (every k_fold); 0: after them (round 5; A/B)
@@ -1570,7 +1577,11 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
         };
         for (uint32_t r = 0; r + 1 < R; ++r) {
             const uint32_t slot = wave_lds + (r & 1u) * kSlotBytes;
-            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            if constexpr (kRoundWait0) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            }
             uint32_t m[32];
             load_line(r, slot, m);
             if (r + 2 < R) {
