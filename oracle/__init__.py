@@ -120,11 +120,44 @@ def time_batch_for(arena, offsets, lengths, nthreads, variant="hw", seconds=0.5,
     return t, reps
 
 
-def pick_cpus(nthreads, numa_node=None):
+def _cpu_busy(sample_s=0.3):
+    """Busy fraction of every CPU over a short window (/proc/stat), {} if
+    unreadable."""
+    import time
+
+    def snap():
+        out = {}
+        with open("/proc/stat") as f:
+            for line in f:
+                if line.startswith("cpu") and line[3].isdigit():
+                    parts = line.split()
+                    v = [int(x) for x in parts[1:]]
+                    idle = v[3] + (v[4] if len(v) > 4 else 0)
+                    out[int(parts[0][3:])] = (sum(v), idle)
+        return out
+    try:
+        a = snap()
+        time.sleep(sample_s)
+        b = snap()
+    except (OSError, ValueError, IndexError):
+        return {}
+    busy = {}
+    for c, (t1, i1) in b.items():
+        t0, i0 = a.get(c, (t1, i1))
+        dt = t1 - t0
+        busy[c] = 1.0 - (i1 - i0) / dt if dt > 0 else 0.0
+    return busy
+
+
+def pick_cpus(nthreads, numa_node=None, avoid_busy=True):
     """Up to nthreads CPUs from this process's allowed set, one per physical
     core (SMT siblings skipped), preferring `numa_node`'s cores (the GPU's
-    node).  Returns the list (shorter if the set holds fewer cores)."""
+    node) and, on a shared host, cores whose threads were idle over a short
+    /proc/stat window (a core another job keeps busy would slow one thread,
+    and with it every window).  Returns the list (shorter if the set holds
+    fewer cores)."""
     allowed = sorted(os.sched_getaffinity(0))
+    busy = _cpu_busy() if avoid_busy else {}
 
     def read(path, default):
         try:
@@ -143,15 +176,19 @@ def pick_cpus(nthreads, numa_node=None):
             pass
         return -1
 
-    seen, first, rest = set(), [], []
+    cores = {}  # physical core -> its allowed CPUs
     for c in allowed:
         topo = "/sys/devices/system/cpu/cpu%d/topology/" % c
         core = (read(topo + "physical_package_id", "0"), read(topo + "core_id", str(c)))
-        if core in seen:
-            continue
-        seen.add(core)
-        (first if numa_node is None or node_of(c) == numa_node else rest).append(c)
-    return (first + rest)[:nthreads]
+        cores.setdefault(core, []).append(c)
+    ranked = []
+    for core, cpus in cores.items():
+        c = cpus[0]
+        load = max(busy.get(x, 0.0) for x in cpus)  # a busy SMT sibling shares the core
+        far = 0 if numa_node is None or node_of(c) == numa_node else 1
+        ranked.append((far, load > 0.1, c, load))
+    ranked.sort()
+    return [r[2] for r in ranked[:nthreads]]
 
 
 def time_repeat(buf, iters, variant="hw"):
