@@ -1199,6 +1199,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     // 1.5 us later, profiles/r05/probe/fold_trace_small_batches.jsonl)
     constexpr bool kEarly = ONE && kOneEarly && WPB == 4;
     static_assert(!kEarly || kTab % (1024 * WPB) == 0, "early tables: whole KiB per wave");
+    constexpr bool kNoVgprTab = kEarly;
     // the wave's first group (claim k = wave, see gid below), as if
     // segment = message: its descriptors are the kernel's first loads
     // (round 6; before, 8-24 KiB of table loads per block went out first
@@ -1209,9 +1210,9 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     if constexpr (kDescFirst) {
         spec = fetch_desc(a, SegRef{sid, 0u}, sid < a.n);
     }
-    uint32_t tw[kEarly ? 1 : kTw];
+    uint32_t tw[kNoVgprTab ? 1 : kTw];
 #pragma unroll
-    for (int i = 0; i < (kEarly ? 0 : kTw); ++i) {
+    for (int i = 0; i < (kNoVgprTab ? 0 : kTw); ++i) {
         const uint32_t t = threadIdx.x + (uint32_t)i * kThreads;
         if constexpr (H11) {
             tw[i] = c_rtab11[t];
@@ -1245,7 +1246,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     // x^(-8p) un-shift table -> LDS too: a per-lane index, so from constant
     // memory it would be a vector load with a full memory latency per group
     __shared__ __attribute__((aligned(16))) uint32_t xneg8[136];
-    const uint32_t xn = (!kEarly && threadIdx.x < 136u) ? c_xneg8[threadIdx.x] : 0u;
+    const uint32_t xn = (!kNoVgprTab && threadIdx.x < 136u) ? c_xneg8[threadIdx.x] : 0u;
     [[maybe_unused]] const uint32_t g0 = blockIdx.x * WPB + wave;  // this wave's index in the grid
     FOLD_STAMP(0)
     if constexpr (!kDescFirst) {
@@ -1254,11 +1255,11 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     // remainder-reduction tables -> LDS (8 KiB, once per block; no DMA in
     // flight yet; plan_reduce's barriers order them before any lookup)
 #pragma unroll
-    for (int i = 0; i < (kEarly ? 0 : kTw); ++i) {
+    for (int i = 0; i < (kNoVgprTab ? 0 : kTw); ++i) {
         const uint32_t t = threadIdx.x + (uint32_t)i * kThreads;
         *(lds_u32*)(uintptr_t)(tab_lds + 4u * t) = tw[i];
     }
-    if (!kEarly && threadIdx.x < 136u) {
+    if (!kNoVgprTab && threadIdx.x < 136u) {
         xneg8[threadIdx.x] = xn;
     }
     // kEarly: this wave's share of the tables, LDS-DMA'd after its first
@@ -1826,25 +1827,22 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
             if (sorted) {
                 r1 = resolve_sorted(r1, v1);
             }
-            if constexpr (!kEarly) {
+            if constexpr (!kNoVgprTab) {
                 nxt = fetch_desc(a, r1, v1);
             }
             const uint32_t s2 = (g + 2u * stride) * 64u + (uint32_t)lane;
             ref2 = map_segment(a, &pl, s2, g + 2u * stride < ngroups && s2 < total, identity, uni,
                                sorted, ep);
             setup(d0, g, G);
-            if constexpr (kEarly) {
-                // a wait the compiler sees (vmcnt(0), expcnt/lgkmcnt free):
-                // none of its loads is pending past here, so its own waits
-                // inside the loop stay where they were (without it, one
-                // landed right after the fold's counted vmcnt(8) and
-                // serialized every group's rounds); nothing but this group's
+            if constexpr (kNoVgprTab) {
+                // a wait the compiler sees (vmcnt(0), expcnt/lgkmcnt free)
+                // before the first asm loads: nothing but this group's
                 // descriptors is in flight yet, so it costs nothing
                 __builtin_amdgcn_s_waitcnt(0x0F70);
             }
             issue_first_rounds(G);
             early_tables();
-            if constexpr (kEarly) {
+            if constexpr (kNoVgprTab) {
                 nxt = fetch_desc(a, r1, v1);  // behind the first data, not in front of it
             }
             FOLD_STAMP(2)
