@@ -103,7 +103,7 @@ struct DevBuf {
 // Planner + staging scratch for one (device, stream).
 struct Workspace {
     std::mutex mu;
-    DevBuf seg_first, block_sum, seginfo, firstk, gdesc, bhist, plan_sync;
+    DevBuf seg_first, block_sum, seginfo, firstk, gdesc, grec, bhist, plan_sync;
     uint32_t plan_epoch = 0;  // k_plan_map launches on this workspace (BatchArgs::plan_epoch)
     uint64_t map_wait_ticks = 10000;  // 100 us (bmqcrc_plan_wait)
 
@@ -264,6 +264,7 @@ int plan_ws(Workspace* w, hipStream_t s, uint64_t n, uint64_t arena_bytes, uint3
         (rc = w->seginfo.ensure(4 * max_segs)) ||
         (rc = w->firstk.ensure(4 * (max_segs / 64 + 2))) ||
         (rc = w->gdesc.ensure(8 * (max_segs / 64 + 2))) ||
+        (rc = w->grec.ensure(32 * (max_segs / 64 + 2))) ||
         (rc = w->bhist.ensure(4ull * kBuckets * kPlanMaxBlocks)) ||
         (rc = w->plan_sync.ensure(8ull * (kSyncFlags + kPlanMaxBlocks +
                                           kPlanMaxBlocks * (kBuckets + 3))))) {
@@ -271,6 +272,9 @@ int plan_ws(Workspace* w, hipStream_t s, uint64_t n, uint64_t arena_bytes, uint3
     }
     if (w->plan_sync.fresh) {  // zero counters, no given-up epoch (stream-ordered)
         HIP_TRY(hipMemsetAsync(w->plan_sync.p, 0, w->plan_sync.bytes, s));
+    }
+    if (w->grec.fresh) {  // no run record of any epoch either
+        HIP_TRY(hipMemsetAsync(w->grec.p, 0, w->grec.bytes, s));
     }
     if (w->gdesc.fresh) {  // no group descriptor of any epoch (epochs start at 1)
         HIP_TRY(hipMemsetAsync(w->gdesc.p, 0, w->gdesc.bytes, s));
@@ -309,6 +313,7 @@ int plan_ws(Workspace* w, hipStream_t s, uint64_t n, uint64_t arena_bytes, uint3
     a->seg_first = (uint32_t*)w->seg_first.p;
     a->firstk = (uint32_t*)w->firstk.p;
     a->gdesc = (unsigned long long*)w->gdesc.p;
+    a->grec = (uint32_t*)w->grec.p;
     a->block_sum = (uint32_t*)w->block_sum.p;
     a->seginfo = (uint32_t*)w->seginfo.p;
     a->bhist = (uint32_t*)w->bhist.p;

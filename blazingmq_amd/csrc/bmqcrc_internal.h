@@ -68,6 +68,9 @@ struct BatchArgs {
                                // each (message, | kSegLast for its last segment)
     uint32_t* firstk;          // workspace, max_segs / 64 + 1: k of each group's first entry
     unsigned long long* gdesc; // workspace, max_segs / 64 + 2 (round 4): (epoch << 32) | message
+    uint32_t* grec;            // workspace, 8 words per group (round 6): the prefix record
+                               // {epoch, message, lanes, 0} and the suffix record, a long
+                               // run's tail and head in the group (k_plan_map)
                                // for a group whose 64 seginfo slots are all full segments of
                                // one message (k_plan_map writes this instead of the 64 entries)
     uint32_t* bhist;           // workspace, kBuckets * nblocks: per-block size-class histogram

@@ -707,6 +707,14 @@ constexpr bool kDescFirst = BMQCRC_DESC_FIRST != 0;
 #define BMQCRC_GROUP_DESC 1  // 0: every seginfo entry written (round 3; A/B)
 #endif
 constexpr bool kGroupDesc = BMQCRC_GROUP_DESC != 0;
+#ifndef BMQCRC_LONG_FLAT
+#define BMQCRC_LONG_FLAT 1  // long runs' entries and descriptors: 1 flattened over the wave, 0 run by run
+#endif
+#ifndef BMQCRC_RUN_RECORDS
+#define BMQCRC_RUN_RECORDS 1  // a long run's partial groups as per-group records, not entries
+                              // (k_plan_map, round 6); 0: entries (round 5; A/B)
+#endif
+constexpr bool kRunRecords = BMQCRC_RUN_RECORDS != 0 && kGroupDesc && BMQCRC_LONG_FLAT;
 
 // The single-pass planner's launch tag.  Normally the host's per-workspace
 // count (BatchArgs::plan_epoch, below 2^31); a batch captured into a graph
@@ -1005,6 +1013,18 @@ __device__ __forceinline__ SegRef map_segment(const BatchArgs& a, const PlanLds*
                 const unsigned long long gd = a.gdesc[gsel];
                 if ((uint32_t)(gd >> 32) == ep) {
                     r.msg = (uint32_t)gd;
+                } else if (kRunRecords) {
+                    // a long run's tail on the group's first lanes, or its
+                    // head on the last ones: tagged records (k_plan_map,
+                    // round 6), the entries under them not written
+                    const u32x4 pre = *(const u32x4*)&a.grec[8u * gsel];
+                    const u32x4 suf = *(const u32x4*)&a.grec[8u * gsel + 4u];
+                    const uint32_t l = seg & 63u;
+                    if (pre.x == ep && l < pre.z) {
+                        r.msg = pre.y;
+                    } else if (suf.x == ep && l >= 64u - suf.z) {
+                        r.msg = suf.y;
+                    }
                 }
             }
         }
@@ -2525,9 +2545,6 @@ constexpr uint32_t kMapRegTiles = BMQCRC_MAP_REG_TILES;  // tiles kept in regist
 #ifndef BMQCRC_PLAN_FLAGS
 #define BMQCRC_PLAN_FLAGS 0  // 1: round 3's separate arrival flags (A/B)
 #endif
-#ifndef BMQCRC_LONG_FLAT
-#define BMQCRC_LONG_FLAT 1  // long runs' entries and descriptors: 1 flattened over the wave, 0 run by run
-#endif
 #ifndef BMQCRC_PLAN_DIAG
 #define BMQCRC_PLAN_DIAG 0  // 3: per-block phase stamps, 4: the same without seginfo stores,
                             // 6: every block's first read of the exchanged words is stale
@@ -3036,12 +3053,49 @@ __global__ __launch_bounds__(kPlanBlock) void k_plan_map(BatchArgs a)
                     const bool whole = kGroupDesc && gf < ge;
                     atv[v] = p;
                     nv[v] = n;
-                    ni[v] = whole ? (64u * gf - p) + (p + n - 64u * ge) : n;
+                    if constexpr (kRunRecords) {
+                        // entries only for a run inside one group touching
+                        // neither of its ends; a run's head (the group's
+                        // last lanes) and tail (its first lanes) are records
+                        const bool inner = n && (p >> 6) == ((p + n - 1u) >> 6) && (p & 63u) &&
+                                           ((p + n) & 63u);
+                        ni[v] = inner ? n : 0u;
+                    } else {
+                        ni[v] = whole ? (64u * gf - p) + (p + n - 64u * ge) : n;
+                    }
                     ng[v] = whole ? ge - gf : 0u;
                     p += n;
                 }
                 *(u32x4*)&slong[w][0][lane * kPlanV] = u32x4{atv[0], atv[1], atv[2], atv[3]};
                 *(u32x4*)&slong[w][1][lane * kPlanV] = u32x4{nv[0], nv[1], nv[2], nv[3]};
+                if constexpr (kRunRecords) {
+                    // Run records (round 6): a long run's partial groups
+                    // are described per group, not per slot -- its head
+                    // (lanes ho..63 of group at/64) by the group's suffix
+                    // record, its tail (lanes 0..te-1 of the last group) by
+                    // the prefix record and firstk; each side of a group has
+                    // one owner (the run covering lane 63, or lane 0).
+                    // Round 5 wrote up to 63 + 63 entries per long run, ~3 MB
+                    // on Zipf's 1/8 shard: 5.3 of its planner's 20.7 us
+                    // (profiles/r05/ab/planner/phase_stamps_fullrun_split.jsonl).
+#pragma unroll
+                    for (uint32_t v = 0; v < kPlanV; ++v) {
+                        const uint32_t at = atv[v], n = nv[v];
+                        if (n == 0u) {
+                            continue;
+                        }
+                        const uint32_t hb = at >> 6, tb = (at + n - 1u) >> 6;
+                        const uint32_t ho = at & 63u, te = (at + n) & 63u;
+                        const uint32_t msg = (uint32_t)(wbase + (uint32_t)lane * kPlanV + v);
+                        if (ho != 0u && (hb < tb || te == 0u)) {
+                            *(u32x4*)&a.grec[8u * hb + 4u] = u32x4{ep, msg, 64u - ho, 0u};
+                        }
+                        if (te != 0u && (hb < tb || ho == 0u)) {
+                            *(u32x4*)&a.grec[8u * tb] = u32x4{ep, msg, te, 0u};
+                            a.firstk[tb] = 64u * tb - at;
+                        }
+                    }
+                }
                 auto flat = [&](const uint32_t (&cnt)[kPlanV], auto&& body) {
                     const uint32_t mine = cnt[0] + cnt[1] + cnt[2] + cnt[3];
                     const uint32_t x = wave_incl_scan(mine);

@@ -708,3 +708,82 @@ def test_long_runs_flat_cover_every_segment(seed):
             assert 64 * g + lane not in got
             got[64 * g + lane] = (q, k0 + lane)
     assert got == want
+
+
+def _long_runs_records(nf, lpos, short=16):
+    """k_plan_map's long runs with run records (round 6, BMQCRC_RUN_RECORDS):
+    whole groups as descriptors, a run's head (the last lanes of its first
+    group) as that group's suffix record, its tail (the first lanes of its
+    last group) as the prefix record with firstk, entries only for a run
+    inside one group touching neither end.  Returns (entries {slot: (run,
+    k)}, groups {g: (run, firstk)}, prefix {g: (run, lanes, firstk)}, suffix
+    {g: (run, lanes)})."""
+    ent, grp, pre, suf = {}, {}, {}, {}
+    p = lpos
+    for q, x in enumerate(nf):
+        n = x if x > short else 0
+        if n:
+            gf, ge = (p + 63) >> 6, (p + n) >> 6
+            for g in range(gf, ge):
+                assert g not in grp
+                grp[g] = (q, 64 * g - p)
+            hb, tb, ho, te = p >> 6, (p + n - 1) >> 6, p & 63, (p + n) & 63
+            if hb == tb and ho and te:
+                for k in range(n):
+                    assert p + k not in ent
+                    ent[p + k] = (q, k)
+            if ho and (hb < tb or te == 0):
+                assert hb not in suf
+                suf[hb] = (q, 64 - ho)
+            if te and (hb < tb or ho == 0):
+                assert tb not in pre
+                pre[tb] = (q, te, 64 * tb - p)
+        p += n
+    return ent, grp, pre, suf
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_run_records_cover_every_segment(seed):
+    """Every full segment of every long run resolves to its (run, k) exactly
+    once the way k_fold reads the map (a group descriptor first, then the
+    prefix record, then the suffix record, else the entry; k of a prefix lane
+    = firstk + lane, of a suffix lane = lane - (64 - lanes)), no record
+    overlaps another or a group descriptor, and every side of a group has at
+    most one owner -- runs aligned to groups, inside one group (touching an
+    end or not) and spanning many."""
+    rng = np.random.default_rng(100 + seed)
+    nf = rng.choice([0, 3, 17, 30, 40, 47, 63, 64, 65, 100, 128, 200, 1000], size=300).tolist()
+    lpos = int(rng.integers(0, 64)) if seed else 0
+    if seed == 1:
+        nf = [64] * 100
+    if seed == 2:
+        nf = [17 + int(i) for i in rng.integers(0, 47, size=300)]  # many runs inside one group
+    ent, grp, pre, suf = _long_runs_records(nf, lpos)
+    want, p = {}, lpos
+    for q, x in enumerate(nf):
+        if x > 16:
+            for k in range(x):
+                want[p + k] = (q, k)
+            p += x
+    got = {}
+    for slot in want:
+        g, lane = slot >> 6, slot & 63
+        if g in grp:
+            q, k0 = grp[g]
+            r = (q, k0 + lane)
+        elif g in pre and lane < pre[g][1]:
+            q, _, k0 = pre[g]
+            r = (q, k0 + lane)
+        elif g in suf and lane >= 64 - suf[g][1]:
+            q, h = suf[g]
+            r = (q, lane - (64 - h))
+        else:
+            r = ent[slot]
+        got[slot] = r
+    assert got == want
+    for g, (q, t, _) in pre.items():
+        assert g not in grp and (g not in suf or t <= 64 - suf[g][1])
+    for slot in ent:
+        g, lane = slot >> 6, slot & 63
+        assert g not in grp
+        assert not (g in pre and lane < pre[g][1]) and not (g in suf and lane >= 64 - suf[g][1])
