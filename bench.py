@@ -208,6 +208,19 @@ def cpu_baseline(lens_np, seed, seconds, device=0):
     if n > 1:
         offs[1:] = csum[:n - 1]
     nbytes = int(lens.sum(dtype=np.uint64))
+    # every thread pinned to its own physical core of the process's allowed
+    # set, on the GPU's NUMA node first, idle cores first (round 6:
+    # unpinned, 16 threads swung 2x between windows of one run);
+    # the 1-thread leg on the first of them.  The sample is written while the
+    # process runs on those cores, so its pages are theirs (first touch).
+    node = gpu_numa_node(device)
+    cpus = oracle.pick_cpus(threads, node)
+    threads = len(cpus)
+    saved_affinity = os.sched_getaffinity(0)
+    try:
+        os.sched_setaffinity(0, cpus)
+    except OSError:
+        pass
     arena = oracle.fill_payload(0, nbytes, seed)
     # a batch far below the sample size (configs[0]: 1,000 x 4 KiB = 4 MB)
     # is tiled to >= 64 MiB, so that a pass is milliseconds of CRC work, not
@@ -220,17 +233,16 @@ def cpu_baseline(lens_np, seed, seconds, device=0):
                 ).reshape(-1)
         lens = np.tile(lens, tiles)
         nbytes *= tiles
-    # every thread pinned to its own physical core of the process's allowed
-    # set, on the GPU's NUMA node first (round 6: unpinned, 16 threads swung
-    # 2x between windows of one run); the 1-thread leg on the
-    # first of them
-    node = gpu_numa_node(device)
-    cpus = oracle.pick_cpus(threads, node)
-    threads = len(cpus)
+    try:
+        os.sched_setaffinity(0, saved_affinity)
+    except OSError:
+        pass
     t1, reps1 = oracle.time_batch_for(arena, offs, lens, 1, "hw", 0.5, cpus=cpus)
-    # the multi-threaded leg shares the box's host with other jobs: seven
-    # timed windows, the median reported with the min and max
+    # the multi-threaded leg shares the box's host with other jobs: one
+    # untimed window (clocks and caches settle), then seven timed windows,
+    # the median reported with the min and max
     nwin = 7
+    oracle.time_batch_for(arena, offs, lens, threads, "hw", max(0.3, seconds / nwin), cpus=cpus)
     legs = [oracle.time_batch_for(arena, offs, lens, threads, "hw", max(0.3, seconds / nwin),
                                   cpus=cpus)
             for _ in range(nwin)]
@@ -255,8 +267,10 @@ def cpu_baseline(lens_np, seed, seconds, device=0):
                         % ((os.cpu_count() or 8) // 8, os.cpu_count() or 0, threads),
         "sample": "first %d msgs (%.0f MiB%s) of the same synthetic batch; %d threads (this "
                   "GPU's share of the host: OMP_NUM_THREADS, 16 per GPU on the pool), each "
-                  "pinned to its own physical core (GPU NUMA node %s first), created once "
-                  "before the clock; median of %d windows of >= %.2f s; single thread %d warm "
+                  "pinned to its own physical core (GPU NUMA node %s first, idle cores first; "
+                  "the sample first-touched there), created once before the clock; one "
+                  "untimed window, then the median of %d windows of >= %.2f s; single "
+                  "thread %d warm "
                   "passes (%.2f s) = %.2f GiB/s; SSE4.2 crc32q 3-way interleaved, lanes joined "
                   "by shift tables (bdlde::Crc32c default analogue, oracle/crc32c_oracle.c); "
                   "host %s, nproc %d"
