@@ -1087,6 +1087,11 @@ __device__ unsigned long long g_fold_trace[kFoldTraceWaves][8];
                            // remainder step, bit 1 the fold; product: 0
 #endif
 
+#ifndef BMQCRC_NT_LOADS
+#define BMQCRC_NT_LOADS 1  // 0: every data round with the default policy (A/B)
+#endif
+constexpr bool kNtLoads = BMQCRC_NT_LOADS != 0;
+
 #ifndef BMQCRC_SHORT_NT_WHOLE_LINES
 #define BMQCRC_SHORT_NT_WHOLE_LINES 1  // 0: every short group with the default policy (round 4)
 #endif
@@ -1552,7 +1557,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
     // non-temporal (round 2).  Round 2 chose the default policy for every
     // short group from a batch the Infinity Cache held (+3 %).
     auto issue_first_rounds = [&](const Group& G) {
-        if (!NT || (kShortDefaultPolicy && G.R <= 2u && !(kShortNtWholeLines && G.whole_lines))) {
+        if (!NT || !kNtLoads || (kShortDefaultPolicy && G.R <= 2u && !(kShortNtWholeLines && G.whole_lines))) {
             dma_round<false>(wave_lds, G.pbase, G.plo, G.pcnt, zero, 0);
             if (G.R > 1) {
                 dma_round<false>(wave_lds + kSlotBytes, G.pbase, G.plo, G.pcnt, zero, 1);
@@ -1606,7 +1611,7 @@ __global__ __launch_bounds__(WPB * 64, WPB == 4 ? 2 : 1) void k_fold(BatchArgs a
             uint32_t m[32];
             load_line(r, slot, m);
             if (r + 2 < R) {
-                dma_round<NT>(slot, G.pbase, G.plo, G.pcnt, zero, r + 2);
+                dma_round<NT && kNtLoads>(slot, G.pbase, G.plo, G.pcnt, zero, r + 2);
             }
             if (ONE && (BMQCRC_ONE_DIAG & 2)) {
 #pragma unroll

@@ -13,8 +13,14 @@ This model counts, for the whole batch and for each strong-scaling shard:
   * shared_lines = lines cut by a message boundary (fetched twice above)
   * meta         = descriptors (12 B/msg), seginfo (4 B/segment) + group
                    descriptors, out (4 B/msg read-modify... counted once)
+  * desc_by_class = the 128-byte lines of `offsets` (8 B/msg) and `lengths`
+                   (4 B/msg) each size class touches, summed over the classes:
+                   k_fold reads descriptors in the sorted map's class order, a
+                   class's messages are sparse in message order, and no cache
+                   keeps a descriptor line from one class to the next (round 6)
 and compares alg + meta + duplicated lines with the measured FETCH/WRITE
-traffic of profiles/rNN/<...>/zipf_4M_summary.json.
+traffic of profiles/rNN/<...>/zipf_4M_summary.json.  With 128-byte aligned
+messages (bench.py --align 128) the same model predicts the aligned run.
 
 usage: python3 tools/zipf_overfetch.py [summary.json] [out.json]
 """
@@ -26,6 +32,35 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+
+
+def size_class(nl):
+    """crc32c_kernels.hip size_class(): 16 buckets, lanes within 1.5x."""
+    nl = nl | 1
+    b = np.floor(np.log2(nl)).astype(np.int64)
+    c = np.where(b > 0, 2 * b + ((nl >> np.maximum(b - 1, 0)) & 1), 0)
+    return np.minimum(c, 15)
+
+
+def desc_by_class(lens, seg=2048, align=0):
+    """Descriptor bytes k_fold fetches when the map is read class by class:
+    per class, the distinct 128-byte lines of offsets and lengths."""
+    lens = lens.astype(np.int64)
+    size = lens if not align else (lens + align - 1) // align * align
+    off = np.zeros(lens.size, dtype=np.int64)
+    np.cumsum(size[:-1], out=off[1:])
+    nseg = (lens + seg - 1) // seg
+    msg = np.repeat(np.arange(lens.size), nseg)
+    k = np.arange(int(nseg.sum())) - np.repeat(np.cumsum(nseg) - nseg, nseg)
+    mo, me = off[msg], off[msg] + lens[msg]
+    S = np.where(k == 0, mo, (mo + k * seg) & ~127)
+    E = np.where(k + 1 == nseg[msg], me, (mo + (k + 1) * seg) & ~127)
+    cls = size_class(((E + 127) >> 7) - (S >> 7))
+    total = 0
+    for c in range(16):
+        m = np.unique(msg[cls == c])
+        total += 128 * (np.unique(m >> 4).size + np.unique(m >> 5).size)
+    return int(total)
 
 
 def model(lens, seg=2048):
@@ -65,10 +100,17 @@ def main():
                            "traffic_over_alg": round(s["traffic_over_alg"], 4),
                            "excess_over_alg": s["traffic_bytes_per_launch"] - s["alg_bytes_per_launch"]}
         w = res["whole"]
+        dbc = desc_by_class(lens)
         res["attribution"] = {
             "metadata": w["meta_bytes"] - 4 * w["msgs"],
             "shared_lines_refetched": w["lines_128_bytes"] - w["payload"],
-            "unexplained": s["traffic_bytes_per_launch"] - w["model_128_total"]}
+            "descriptor_rereads_by_class": dbc - 12 * w["msgs"],
+            "unexplained": s["traffic_bytes_per_launch"] - w["model_128_total"]
+            - (dbc - 12 * w["msgs"])}
+        # the same batch with every message 128-byte aligned: no shared lines
+        la = lens.astype(np.int64)
+        res["aligned_128_model"] = int(((la + 127) // 128 * 128).sum()) + w["meta_bytes"] \
+            + desc_by_class(lens, align=128) - 12 * w["msgs"]
     print(json.dumps(res, indent=1))
     if len(sys.argv) > 2:
         with open(sys.argv[2], "w") as f:
