@@ -678,6 +678,52 @@ def test_speculative_single_launch(cuda):
         run(lens, tag)
 
 
+def test_one_segment_many_rows(cuda):
+    """The 8-wave one-segment kernel over many rows of groups: 1.5M messages
+    are 12 groups per wave on 256 CUs.  Repeated launches on one stream, a
+    second stream's workspace in between, and mispredicted long messages in
+    the first rows and (3,000 of them) in the last third, folded by the
+    waves' second pass, are all bit-exact; every speculative batch is one
+    launch.  (Round 6 A/B'd a dynamic tail for this kernel against it.)"""
+    import torch
+    from blazingmq_amd.crc32c import last_launch
+    rng = np.random.default_rng(1515)
+    arena_np = rng.integers(0, 256, size=64 << 20, dtype=np.uint8)
+    arena = torch.from_numpy(arena_np).to(cuda)
+    s1, s2 = torch.cuda.Stream(cuda), torch.cuda.Stream(cuda)
+    n = 1_500_000
+
+    def run(lens, tag, s):
+        lens = np.asarray(lens, np.uint32)
+        offs = np.array(rng.integers(0, arena_np.size - lens.astype(np.int64) + 1), np.int64)
+        seeds = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+        got = Crc32c.calculate_batch(arena, torch.from_numpy(offs).to(cuda),
+                                     torch.from_numpy(lens.view(np.int32)).to(cuda),
+                                     torch.from_numpy(seeds.view(np.int32)).to(cuda), stream=s)
+        s.synchronize()
+        exp = oracle.batch(arena_np, offs, lens, seeds, nthreads=8)
+        bad = np.nonzero(got.cpu().numpy().view(np.uint32) != exp)[0]
+        assert bad.size == 0, (tag, bad.size, [(int(i), int(lens[i])) for i in bad[:8]])
+        return last_launch(cuda.index, s)
+
+    short = lambda: rng.integers(1, 257, size=n)  # noqa: E731  (one segment each: identity)
+    run(short(), "planned", s1)
+    for k in range(3):
+        ll = run(short(), "spec %d" % k, s1)
+        assert ll["spec"] == 1 and ll["kernels"] == 1, ll
+        if k == 1:
+            run(short(), "other stream", s2)
+    mixed = short()
+    tail = np.arange(n - n // 3, n)
+    where = np.concatenate([rng.choice(tail, size=3000, replace=False),
+                            rng.integers(0, n - n // 3, size=200)])
+    mixed[where] = rng.integers(300, 20_000, size=where.size)
+    run(mixed, "spec mispredicted in the tail", s1)
+    run(short(), "planned again", s1)
+    ll = run(short(), "spec after", s1)
+    assert ll["spec"] == 1, ll
+
+
 @pytest.mark.parametrize("n", [1_000, 100_003, 600_000])
 def test_one_segment_pipeline_shapes(cuda, n):
     """The one-segment kernel (every message declared to fit one segment):
