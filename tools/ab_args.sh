@@ -12,7 +12,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 prefix=$1
 variants=$2
 shift 2
-mkdir -p gpurun_out
+mkdir -p gpurun_out "$(dirname gpurun_out/$prefix)"
 out=gpurun_out/$prefix.jsonl
 : > "$out"
 lib=blazingmq_amd/lib
