@@ -72,3 +72,9 @@ def test_cpu_baseline_states_its_thread_counts():
     assert cb["kind"] == "port" and cb["value"] > 0 and cb["single_thread_value"] > 0
     assert cb["cores"] == bench.host_threads() and cb["host_threads"] == os.cpu_count()
     assert "nproc/8" in cb["not_measured"]
+    # the value is the cache-resident median of seven windows, the streamed
+    # leg reported beside it
+    assert len(cb["windows_GiBps"]) == 7 and len(cb["streamed_windows_GiBps"]) == 7
+    assert cb["value"] == sorted(cb["windows_GiBps"])[3]
+    assert cb["streamed_value"] == sorted(cb["streamed_windows_GiBps"])[3]
+    assert "cache-resident" in cb["sample"]
