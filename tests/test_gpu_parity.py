@@ -420,6 +420,54 @@ def test_shape_hint_misprediction(cuda):
 
 
 @pytest.mark.perf
+def test_auto_2k_batch_every_planner_path(cuda):
+    """An automatically sized 2 KiB batch (>= 512 MiB of arena) of 1.5M short
+    messages with long ones mixed in -- lengths on either side of 64 KiB and
+    of 4 KiB multiples up to 1 MiB, seeds -- bit-exact through every planner
+    path: the light planner's search, the size-class map (past four tiles
+    per block: register and reloaded tiles), a given-up map, and the
+    host-buffer call that sees the lengths.  (Round 6 ran a two-tier
+    segmentation experiment against it, Appendix A.)"""
+    import torch
+    from blazingmq_amd import last_launch, plan_wait
+    rng = np.random.default_rng(2024)
+    arena_np = rng.integers(0, 256, size=640 << 20, dtype=np.uint8)
+    arena = torch.from_numpy(arena_np).to(cuda)
+    edges = np.array([65535, 65536, 65537, 65536 + 4095, 65536 + 4096, 65536 + 4097,
+                      2 * 65536 - 1, 4096 * 63, 4096 * 64 + 1, 1 << 20], np.uint32)
+    lens = np.concatenate([rng.integers(1, 2048, size=1_500_000),
+                           rng.integers(4096, 65536, size=3000),
+                           rng.integers(65536, 600_000, size=1500),
+                           np.repeat(edges, 20)]).astype(np.uint32)
+    rng.shuffle(lens)
+    offs = (rng.random(lens.size) * (arena_np.size - lens + 1)).astype(np.int64)
+    seeds = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64).astype(np.uint32)
+    exp = oracle.batch(arena_np, offs, lens, seeds, nthreads=8)
+    d_offs = torch.from_numpy(offs).to(cuda)
+    d_lens = torch.from_numpy(lens.view(np.int32)).to(cuda)
+    d_seeds = torch.from_numpy(seeds.view(np.int32)).to(cuda)
+    s = torch.cuda.Stream(cuda)
+
+    def check(tag):
+        got = Crc32c.calculate_batch(arena, d_offs, d_lens, d_seeds, stream=s)
+        s.synchronize()
+        bad = np.nonzero(got.cpu().numpy().view(np.uint32) != exp)[0]
+        assert bad.size == 0, (tag, bad.size, [(int(i), int(lens[i])) for i in bad[:6]])
+        return last_launch(cuda.index, s)
+
+    ll = check("first batch (light planner, search)")
+    assert ll["seg_bytes"] == 2048, ll
+    ll = check("size-class map")
+    assert ll["map"] == 1, ll
+    check("map again")
+    plan_wait(cuda.index, s, 0)
+    check("map given up")
+    plan_wait(cuda.index, s, 100)
+    check("mapped after")
+    got = Crc32c.calculate_batch(arena_np, offs, lens, seeds)
+    assert np.array_equal(np.asarray(got).view(np.uint32), exp)
+
+
 def test_planner_map_given_up(cuda, record_property, perf_bound):
     # Ragged batches are planned by one kernel whose blocks meet once,
     # grid-wide.  When they cannot all run at once a block stops waiting after
